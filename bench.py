@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Headline benchmark: simulated instructions/second of 8-node DASH systems.
+
+Workload (BASELINE.json configs[2], the `metric`'s configuration): 1M (2^20)
+independent 8-node systems per GPU, 4096 uniform-random RD/WR per node,
+CACHE_SIZE 4. Traces are generated on the device (counter-based, seed keyed
+by the GLOBAL system id) before the timed region, so they are resident in
+HBM (64 GiB per GPU). One step = one full pass of the hot path: every system
+from initial state to quiescence.
+
+Multi-GPU: one process per GPU (torchrun). Systems are sharded by global id
+with no data-path collective (weak scaling); the single exchange is one RCCL
+all-reduce of the per-transaction histograms after the timed region.
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+PEAK_HBM = 8.0e12  # B/s, MI355X_MICROARCH.md chip table
+BYTES_PER_INSTR = 2  # packed trace record read once
+
+
+def load_dash():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "dash_amd", ROOT / "ue22cs343bb1-openmp-assignment_amd" / "dash.py")
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["dash_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def cpu_baseline(args, seed, kind, locality, target_s):
+    """The oracle (C port of the reference protocol, OpenMP over systems) on a
+    bounded sample of the same workload, on this box's host cores."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ctypes as oc
+    threads = args.cpu_threads
+    cal = oc.run_batch(seed, 0, max(threads, 8), num_procs=8, cache_size=args.cache_size,
+                       length=args.len, kind=kind, locality=locality, threads=threads)
+    rate = cal["instructions"] / max(cal["seconds"], 1e-9)
+    per_sys = 8 * args.len
+    count = int(max(threads, min(1 << 20, rate * target_s / per_sys)))
+    res = oc.run_batch(seed, 0, count, num_procs=8, cache_size=args.cache_size, length=args.len,
+                       kind=kind, locality=locality, threads=threads)
+    return {"value": res["instructions"] / res["seconds"], "unit": "instr/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{count} systems x 8 nodes x {args.len} instr ({args.kind}, CS={args.cache_size}, "
+                      f"seed 0x{seed:X}) in {res['seconds']:.1f} s on {threads} threads; "
+                      f"oracle/dash_oracle.c lockstep restatement of assignment.c"}
+
+
+def read_traffic(kind):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    f = ROOT / "profiles" / f"traffic_{kind}.json"
+    if f.exists():
+        try:
+            return json.loads(f.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--systems", type=int, default=1 << 20, help="systems per GPU")
+    ap.add_argument("--len", type=int, default=4096, help="instructions per node")
+    ap.add_argument("--cache-size", type=int, default=4)
+    ap.add_argument("--kind", choices=["uniform", "contention", "locality"], default="uniform")
+    ap.add_argument("--locality", type=float, default=0.5)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    dash = load_dash()
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    kind = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
+            "locality": dash.GEN_LOCALITY}[args.kind]
+    locality = int(round(args.locality * 65536)) if args.kind == "locality" else 0
+    M = args.systems
+    eng = dash.Engine(M, num_procs=8, cache_size=args.cache_size, max_instr=args.len,
+                      device=local_rank)
+    eng.generate(args.seed, args.len, kind=kind, locality=locality, sys_base=rank * M)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        eng.run()
+    barrier()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    stats = None
+    for _ in range(args.steps):
+        stats = eng.run()
+        kernel_ms.append(stats["kernel_ms"])
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    dev = torch.device("cuda", local_rank)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    hist = torch.tensor(stats["hist"] + [stats["instructions"], stats["rounds_total"],
+                                         stats["err_systems"], stats["dropped"]],
+                        dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM)  # the one RCCL exchange
+    elapsed = float(t.item())
+    totals = hist.tolist()
+
+    instr_per_step = world * M * 8 * args.len
+    value = instr_per_step * args.steps / elapsed
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    achieved = M * 8 * args.len * BYTES_PER_INSTR / avg_kernel_s
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, args.seed, kind, locality, args.cpu_seconds)
+        line = {
+            "metric": "simulated instr/sec (whole node), 8-core DASH systems; % HBM roofline",
+            "value": value,
+            "unit": "instr/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (on-device counter-based generator, seed keyed by global system id)",
+            "config": {"workload": f"{M} systems/GPU x 8 nodes x {args.len} {args.kind} RD/WR per node, "
+                                   f"CACHE_SIZE={args.cache_size}",
+                       "systems_per_gpu": M, "num_procs": 8, "instr_per_node": args.len,
+                       "cache_size": args.cache_size, "trace": args.kind,
+                       "parallelism": f"systems sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM,
+                         "traffic": read_traffic(args.kind)},
+            "cpu_baseline": cpu,
+            "kernel_ms_avg": avg_kernel_s * 1e3,
+            "totals": {"hist": totals[:13], "instructions_per_step": totals[13],
+                       "rounds_total": totals[14], "err_systems": totals[15], "dropped": totals[16]},
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

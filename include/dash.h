@@ -1,0 +1,159 @@
+/*
+ * dash.h -- C-ABI of libdash, the MI355X batched DASH directory-coherence
+ * simulator (drop-in for the hot path of vibhav950/UE22CS343BB1-OpenMP-Assignment).
+ *
+ * The reference (assignment.c) simulates ONE system of NUM_PROCS nodes with
+ * one OpenMP thread per node. libdash simulates up to millions of independent
+ * systems per GPU under the deterministic lockstep schedule,
+ * one wave64 lane per node. Plain pointers and sizes only; no torch types.
+ *
+ * Reference interfaces each entry point replaces (file:line in assignment.c):
+ *   dash_parse_core_file   initializeProcessor's trace parse         :822-850
+ *   dash_init_node_state   initializeProcessor's state init          :806-821
+ *   dash_load_traces/_dir  per-thread traces in processorNode        :89-95, :152
+ *   dash_run               the OpenMP parallel region: event loop,
+ *                          13-way dispatch, sendMessage,
+ *                          handleCacheReplacement, locks/queues      :135-155, :149-738,
+ *                                                                    :741-765, :767-804
+ *   dash_read_state        the private processorNode after the run   :145, :149
+ *   dash_dump_node/_file   printProcessorState                       :853-905
+ *   dash_simulate_dir      main() end to end                         :126-739
+ *
+ * Errors: negative return codes (DASH_E*); nothing exits or throws across the
+ * ABI. Per-system protocol faults are reported as DASH_ERR_* bits.
+ */
+#ifndef DASH_H
+#define DASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DASH_MEM_SIZE 16   /* MEM_SIZE (ref :8) */
+#define DASH_MAX_PROCS 8   /* bitVector is one byte (ref :63) */
+#define DASH_MAX_CACHE 16
+#define DASH_RING_DEPTH 32 /* per-node LDS queue (ref MSG_BUFFER_SIZE 256, :9) */
+#define DASH_NUM_TXN 13    /* transactionType (ref :30-44) */
+
+/* return codes */
+#define DASH_OK 0
+#define DASH_EINVAL -1   /* bad argument / configuration */
+#define DASH_EIO -2      /* trace file missing or unreadable (ref :826-828) */
+#define DASH_EPARSE -3   /* a line the reference would turn into garbage */
+#define DASH_EADDR -4    /* trace address homed on a node >= num_procs */
+#define DASH_EDEVICE -5  /* HIP runtime error (no device, launch failure, ...) */
+#define DASH_ENOMEM -6
+#define DASH_ESTATE -7   /* call out of order (e.g. read_state before run) */
+
+/* per-system protocol fault bits (reference UB made defined) */
+#define DASH_ERR_OVERFLOW 1u  /* receiver queue full: dropped (ref :754-761) */
+#define DASH_ERR_OOB 2u       /* receiver >= N: dropped (ref :751 via :772,786) */
+#define DASH_ERR_CTZ0 4u      /* ctz(0) on an EM entry: dropped (ref :209,451) */
+#define DASH_ERR_DEADLOCK 8u  /* quiescent with a node still waiting */
+#define DASH_ERR_ROUNDCAP 16u /* stopped at max_rounds */
+
+/* transactionType ordinals (ref :30-44) */
+enum dash_txn {
+    DASH_READ_REQUEST, DASH_WRITE_REQUEST, DASH_REPLY_RD, DASH_REPLY_WR, DASH_REPLY_ID,
+    DASH_INV, DASH_UPGRADE, DASH_WRITEBACK_INV, DASH_WRITEBACK_INT, DASH_FLUSH,
+    DASH_FLUSH_INVACK, DASH_EVICT_SHARED, DASH_EVICT_MODIFIED
+};
+
+/* flags */
+#define DASH_KEEP_STATE 1u /* write full final node state (needed by dash_read_state) */
+
+typedef struct dash_cfg {
+    uint32_t num_procs;   /* NUM_PROCS (ref :6): 4 or 8 */
+    uint32_t cache_size;  /* CACHE_SIZE (ref :7): 1, 2, 4, 8 or 16 */
+    uint32_t max_instr;   /* longest trace per node (ref MAX_INSTR_NUM 32, :10) */
+    uint32_t flags;       /* DASH_KEEP_STATE */
+    uint64_t num_systems; /* independent systems in the batch */
+    uint64_t max_rounds;  /* per-system round cap; 0 = 1024 + 256*max_instr */
+    int32_t device;       /* HIP device ordinal */
+    uint32_t _reserved;
+} dash_cfg;
+
+/* Final node state in the reference's own terms (processorNode, ref :89-95). */
+typedef struct dash_node_state {
+    uint8_t memory[DASH_MEM_SIZE];
+    uint8_t dir_bitvector[DASH_MEM_SIZE];
+    uint8_t dir_state[DASH_MEM_SIZE];     /* EM=0, S=1, U=2 (ref :28) */
+    uint8_t cache_addr[DASH_MAX_CACHE];
+    uint8_t cache_value[DASH_MAX_CACHE];
+    uint8_t cache_state[DASH_MAX_CACHE];  /* MODIFIED=0 .. INVALID=3 (ref :17) */
+} dash_node_state;
+
+typedef struct dash_stats {
+    uint64_t hist[DASH_NUM_TXN]; /* messages handled per transactionType */
+    uint64_t instructions;       /* instructions issued */
+    uint64_t rounds_total;       /* sum over systems of lockstep rounds */
+    uint64_t rounds_max;
+    uint64_t systems;
+    uint64_t err_systems;        /* systems with any DASH_ERR_* bit */
+    uint64_t err_bits;           /* OR of all DASH_ERR_* bits */
+    uint64_t dropped;            /* messages dropped */
+    uint64_t max_depth;          /* deepest queue after any delivery */
+    double kernel_ms;            /* simulation kernel time (HIP events, engine stream) */
+} dash_stats;
+
+/* Synthetic trace generator (counter-based, identical host spec in DESIGN.md §gen). */
+#define DASH_GEN_UNIFORM 0u
+#define DASH_GEN_CONTENTION 1u /* 90 %: WR to 0x00..0x03 (homed on node 0) */
+#define DASH_GEN_LOCALITY 2u   /* node == own w.p. locality/65536, else another node */
+typedef struct dash_gen {
+    uint64_t seed;
+    uint64_t sys_base;  /* global id of this handle's system 0 (multi-GPU sharding) */
+    uint32_t kind;
+    uint32_t locality;
+    uint32_t len;       /* instructions per node (<= cfg.max_instr) */
+    uint32_t _reserved;
+} dash_gen;
+
+typedef struct dash_ctx dash_t;
+
+/* ---- lifecycle / device path (libdash.so, HIP) ---- */
+int dash_create(const dash_cfg *cfg, dash_t **out);
+void dash_destroy(dash_t *h);
+const char *dash_last_error(const dash_t *h);
+
+/* traces: packed u16 (bit15 = WR, bits 14..8 = address, bits 7..0 = value),
+   layout [sys][node][stride]; lens[sys*num_procs + node] */
+int dash_load_traces(dash_t *h, const uint16_t *packed, uint64_t stride, const uint32_t *lens,
+                     uint64_t num_systems);
+int dash_generate(dash_t *h, const dash_gen *g);
+int dash_run(dash_t *h, dash_stats *stats);
+int dash_read_state(dash_t *h, uint64_t sys, dash_node_state *out /* [num_procs] */);
+int dash_read_results(dash_t *h, uint64_t first, uint64_t count, uint64_t *digests,
+                      uint32_t *rounds, uint32_t *errors);
+int dash_read_hist(dash_t *h, uint64_t sys, uint32_t *hist /* [DASH_NUM_TXN] */);
+/* HIP stream the engine launches on (hipStream_t as void*) */
+void *dash_stream(dash_t *h);
+
+/* ---- host boundary (pure C, no device) ---- */
+/* initializeProcessor's parse (ref :822-850): up to max_instr records into out[]. */
+int dash_parse_core_file(const char *path, uint32_t num_procs, uint32_t max_instr,
+                         uint16_t *out, uint32_t *len);
+/* Resolve the reference's `tests/<dir>/core_<n>.txt` rule (ref :824); also accepts a
+   directory that directly holds core_<n>.txt. Writes the resolved path. */
+int dash_resolve_dir(const char *dir, char *resolved, size_t cap);
+int dash_load_dir(dash_t *h, const char *dir, uint64_t sys);
+void dash_init_node_state(dash_node_state *s, uint32_t node_id, uint32_t cache_size);
+/* printProcessorState byte-exact (ref :853-905). Returns bytes written, or < 0. */
+int dash_dump_node(const dash_node_state *s, uint32_t node_id, uint32_t cache_size, char *buf,
+                   size_t cap);
+int dash_dump_file(const dash_node_state *s, uint32_t node_id, uint32_t cache_size,
+                   const char *path);
+uint64_t dash_digest_node(const dash_node_state *s, uint32_t node_id, uint32_t cache_size);
+/* main() end to end for one system: parse dir, run on the GPU, write
+   core_<n>_output.txt into out_dir (ref :126-739, :860). */
+int dash_simulate_dir(const char *dir, uint32_t num_procs, uint32_t cache_size,
+                      uint32_t max_instr, const char *out_dir, int device, dash_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,628 @@
+/*
+ * dash_oracle.c -- TEST INFRASTRUCTURE ONLY (parity checker, never shipped).
+ *
+ * Sequential restatement of /root/reference/assignment.c's per-node event
+ * loop (:149-738), sendMessage (:741-765) and handleCacheReplacement
+ * (:767-804), driven by the deterministic lockstep schedule of SURVEY.md
+ * App. C:
+ *   - every round, each node takes ONE step on start-of-round state: pop and
+ *     handle one message if its queue is non-empty (ref :167-619), else issue
+ *     one instruction if it is not waiting and has instructions left
+ *     (ref :624-735), else idle;
+ *   - messages sent during the round are appended to the receivers' queues at
+ *     the end of the round, ascending sender id, program order within a sender;
+ *   - the system is quiescent when every queue is empty and no node can issue.
+ * Defined behaviour where the reference is undefined (SURVEY.md App. B 5,8,9):
+ * a send to a node >= N, ctz(0) and queue overflow drop the message and raise
+ * an error bit.
+ *
+ * The code mirrors the reference's control structure handler by handler (no
+ * packing, no predication) so it can be read side by side with
+ * assignment.c; the GPU kernel is a different, predicated formulation.
+ */
+#include "dash_oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* cacheLineState (ref :17), directoryEntryState (ref :28), transactionType (ref :30-44) */
+enum { MODIFIED, EXCLUSIVE, SHARED, INVALID };
+enum { EM, S, U };
+enum {
+    READ_REQUEST, WRITE_REQUEST, REPLY_RD, REPLY_WR, REPLY_ID, INV, UPGRADE,
+    WRITEBACK_INV, WRITEBACK_INT, FLUSH, FLUSH_INVACK, EVICT_SHARED, EVICT_MODIFIED
+};
+
+#define MAX_RING 256
+#define MAX_OUT (ORC_MAX_PROCS + 4)
+
+typedef struct {
+    uint8_t type, sender, address, value, bitVector, secondReceiver, dirState;
+} omsg; /* message (ref :70-79) */
+
+typedef struct {
+    uint8_t address, value, state;
+} oline; /* cacheLine (ref :56-60) */
+
+typedef struct {
+    oline cache[ORC_MAX_CACHE];
+    uint8_t memory[ORC_MEM_SIZE];
+    uint8_t bitVector[ORC_MEM_SIZE];
+    uint8_t dirState[ORC_MEM_SIZE];
+    const uint16_t *trace;
+    uint32_t count; /* instructionCount */
+    uint32_t idx;   /* next instruction to issue */
+    int waiting;    /* waitingForReply (ref :162) */
+    uint8_t instr_type, instr_address, instr_value; /* `instr` (ref :159), last issued */
+    /* incoming queue (messageBuffer, ref :81-87) */
+    omsg q[MAX_RING];
+    uint32_t head, qcount;
+    /* this round's sends, in program order */
+    int nout;
+    int out_to[MAX_OUT];
+    omsg out[MAX_OUT];
+} onode;
+
+typedef struct {
+    int N, CS, ring;
+    onode node[ORC_MAX_PROCS];
+    orc_result *res;
+    char *log;
+    uint64_t log_len, log_cap;
+} osys;
+
+/* sendMessage (ref :741-765), deferred to the end of the round */
+static void send_message(onode *nd, int receiver, omsg m) {
+    nd->out_to[nd->nout] = receiver;
+    nd->out[nd->nout] = m;
+    nd->nout++;
+}
+
+/* handleCacheReplacement (ref :767-804) */
+static void handle_cache_replacement(onode *nd, int sender, oline old) {
+    int home = (old.address >> 4) & 0x0F;
+    omsg m = {0};
+    switch (old.state) {
+    case EXCLUSIVE:
+    case SHARED:
+        m.type = EVICT_SHARED;
+        m.sender = (uint8_t)sender;
+        m.address = old.address;
+        send_message(nd, home, m);
+        break;
+    case MODIFIED:
+        m.type = EVICT_MODIFIED;
+        m.sender = (uint8_t)sender;
+        m.address = old.address;
+        m.value = old.value;
+        send_message(nd, home, m);
+        break;
+    default: /* INVALID: no action (ref :800-802) */
+        break;
+    }
+}
+
+static int ctz8(uint8_t v) { return __builtin_ctz((unsigned)v); }
+
+/* One message through the 13-way dispatch (ref :186-618). */
+static void handle_message(osys *sy, int tid, omsg msg) {
+    onode *nd = &sy->node[tid];
+    const int CS = sy->CS;
+    uint8_t procNodeAddr = (msg.address >> 4) & 0x0F; /* ref :186-188 */
+    uint8_t memBlockAddr = msg.address & 0x0F;
+    uint8_t cacheIndex = memBlockAddr % CS;
+    oline *L = &nd->cache[cacheIndex];
+    omsg r = {0};
+
+    sy->res->hist[msg.type]++;
+    switch (msg.type) {
+    case READ_REQUEST: /* ref :191-237 */
+        if (nd->dirState[memBlockAddr] == EM) {
+            if (nd->bitVector[memBlockAddr] == 0) { sy->res->errors |= ORC_ERR_CTZ0; sy->res->dropped++; break; }
+            r.type = WRITEBACK_INT;
+            r.sender = (uint8_t)tid;
+            r.address = msg.address;
+            r.secondReceiver = msg.sender;
+            send_message(nd, ctz8(nd->bitVector[memBlockAddr]), r);
+        } else if (nd->dirState[memBlockAddr] == S) {
+            r.type = REPLY_RD;
+            r.sender = (uint8_t)tid;
+            r.address = msg.address;
+            r.value = nd->memory[memBlockAddr];
+            r.dirState = S;
+            send_message(nd, msg.sender, r);
+            nd->bitVector[memBlockAddr] |= (uint8_t)(1u << msg.sender);
+        } else { /* U */
+            r.type = REPLY_RD;
+            r.sender = (uint8_t)tid;
+            r.address = msg.address;
+            r.value = nd->memory[memBlockAddr];
+            r.dirState = EM;
+            send_message(nd, msg.sender, r);
+            nd->dirState[memBlockAddr] = EM;
+            nd->bitVector[memBlockAddr] = (uint8_t)(1u << msg.sender);
+        }
+        break;
+
+    case REPLY_RD: /* ref :239-255 */
+        if (L->address != msg.address && L->state != INVALID)
+            handle_cache_replacement(nd, tid, *L);
+        L->address = msg.address;
+        L->value = msg.value;
+        L->state = (msg.dirState == S) ? SHARED : EXCLUSIVE;
+        nd->waiting = 0;
+        break;
+
+    case WRITEBACK_INT: /* ref :257-286; reads/changes cache[idx] with no address check */
+        r.type = FLUSH;
+        r.sender = (uint8_t)tid;
+        r.address = msg.address;
+        r.value = L->value;
+        r.secondReceiver = msg.secondReceiver;
+        send_message(nd, procNodeAddr, r);
+        if (procNodeAddr != msg.secondReceiver)
+            send_message(nd, msg.secondReceiver, r);
+        L->state = SHARED;
+        break;
+
+    case FLUSH: /* ref :288-323 */
+        if (tid == procNodeAddr) {
+            nd->dirState[memBlockAddr] = S;
+            nd->bitVector[memBlockAddr] |= (uint8_t)(1u << msg.secondReceiver);
+            nd->memory[memBlockAddr] = msg.value;
+        }
+        if (tid == msg.secondReceiver) {
+            if (L->address != msg.address && L->state != INVALID)
+                handle_cache_replacement(nd, tid, *L);
+            L->address = msg.address;
+            L->value = msg.value;
+            L->state = SHARED;
+        }
+        nd->waiting = 0; /* unconditional (App. B 2) */
+        break;
+
+    case UPGRADE: { /* ref :325-349; no directory-state check */
+        uint8_t others = nd->bitVector[memBlockAddr] & (uint8_t)~(1u << msg.sender);
+        r.type = REPLY_ID;
+        r.sender = (uint8_t)tid;
+        r.address = msg.address;
+        r.bitVector = others;
+        send_message(nd, msg.sender, r);
+        nd->dirState[memBlockAddr] = EM;
+        nd->bitVector[memBlockAddr] = (uint8_t)(1u << msg.sender);
+        break;
+    }
+
+    case REPLY_ID: /* ref :351-387; fills with the last issued instr.value */
+        for (int i = 0; i < sy->N; i++) {
+            if (msg.bitVector & (1u << i)) {
+                omsg inv = {0};
+                inv.type = INV;
+                inv.sender = (uint8_t)tid;
+                inv.address = msg.address;
+                send_message(nd, i, inv);
+            }
+        }
+        if (L->address != msg.address && L->state != INVALID)
+            handle_cache_replacement(nd, tid, *L);
+        L->address = msg.address;
+        L->value = nd->instr_value;
+        L->state = MODIFIED;
+        nd->waiting = 0;
+        break;
+
+    case INV: /* ref :389-399; state not checked */
+        if (L->address == msg.address)
+            L->state = INVALID;
+        break;
+
+    case WRITE_REQUEST: /* ref :401-459 */
+        if (nd->dirState[memBlockAddr] == U) {
+            r.type = REPLY_WR;
+            r.sender = (uint8_t)tid;
+            r.address = msg.address;
+            send_message(nd, msg.sender, r);
+        } else if (nd->dirState[memBlockAddr] == S) {
+            r.type = REPLY_ID;
+            r.sender = (uint8_t)tid;
+            r.address = msg.address;
+            r.bitVector = nd->bitVector[memBlockAddr] & (uint8_t)~(1u << msg.sender);
+            send_message(nd, msg.sender, r);
+        } else { /* EM */
+            if (nd->bitVector[memBlockAddr] == 0) {
+                sy->res->errors |= ORC_ERR_CTZ0;
+                sy->res->dropped++;
+            } else {
+                r.type = WRITEBACK_INV;
+                r.sender = (uint8_t)tid;
+                r.address = msg.address;
+                r.value = msg.value;
+                r.secondReceiver = msg.sender;
+                send_message(nd, ctz8(nd->bitVector[memBlockAddr]), r);
+            }
+        }
+        nd->dirState[memBlockAddr] = EM; /* ref :456-457, every branch */
+        nd->bitVector[memBlockAddr] = (uint8_t)(1u << msg.sender);
+        break;
+
+    case REPLY_WR: /* ref :461-474; replacement is unconditional (App. B 6) */
+        handle_cache_replacement(nd, tid, *L);
+        L->address = msg.address;
+        L->value = nd->instr_value;
+        L->state = MODIFIED;
+        nd->waiting = 0;
+        break;
+
+    case WRITEBACK_INV: /* ref :476-503; FLUSH_INVACK twice when home == requester */
+        r.type = FLUSH_INVACK;
+        r.sender = (uint8_t)tid;
+        r.address = msg.address;
+        r.value = L->value;
+        r.secondReceiver = msg.secondReceiver;
+        send_message(nd, procNodeAddr, r);
+        send_message(nd, msg.secondReceiver, r);
+        L->state = INVALID;
+        break;
+
+    case FLUSH_INVACK: /* ref :505-536 */
+        if (tid == procNodeAddr) {
+            nd->bitVector[memBlockAddr] = (uint8_t)(1u << msg.secondReceiver);
+            nd->memory[memBlockAddr] = msg.value;
+        }
+        if (tid == msg.secondReceiver) {
+            if (L->address != msg.address && L->state != INVALID)
+                handle_cache_replacement(nd, tid, *L);
+            L->address = msg.address;
+            L->value = nd->instr_value;
+            L->state = MODIFIED;
+        }
+        nd->waiting = 0;
+        break;
+
+    case EVICT_SHARED: /* ref :538-590 */
+        if (tid != procNodeAddr) {
+            L->state = EXCLUSIVE; /* no address check (App. B 5) */
+        } else {
+            nd->bitVector[memBlockAddr] &= (uint8_t)~(1u << msg.sender);
+            int numSharers = __builtin_popcount(nd->bitVector[memBlockAddr]);
+            if (numSharers == 0) {
+                nd->dirState[memBlockAddr] = U;
+            } else if (numSharers == 1) {
+                nd->dirState[memBlockAddr] = EM;
+                int newOwner = ctz8(nd->bitVector[memBlockAddr]);
+                if (newOwner != procNodeAddr) {
+                    r.type = EVICT_SHARED;
+                    r.sender = (uint8_t)tid;
+                    r.address = msg.address;
+                    r.value = nd->memory[memBlockAddr];
+                    send_message(nd, newOwner, r);
+                } else {
+                    L->state = EXCLUSIVE;
+                }
+            }
+        }
+        break;
+
+    case EVICT_MODIFIED: /* ref :592-617 */
+        nd->memory[memBlockAddr] = msg.value;
+        nd->bitVector[memBlockAddr] = 0;
+        nd->dirState[memBlockAddr] = U;
+        break;
+    }
+}
+
+/* Issue one instruction (ref :647-735). */
+static void issue_instruction(osys *sy, int tid) {
+    onode *nd = &sy->node[tid];
+    uint16_t w = nd->trace[nd->idx++];
+    uint8_t type = (w & 0x8000) ? 'W' : 'R';
+    uint8_t address = (uint8_t)((w >> 8) & 0x7F);
+    uint8_t value = (uint8_t)(w & 0xFF);
+    nd->instr_type = type;
+    nd->instr_address = address;
+    nd->instr_value = value;
+    sy->res->instructions++;
+
+    if (sy->log && sy->log_len + 64 < sy->log_cap) /* DEBUG_INSTR (ref :650-651) */
+        sy->log_len += (uint64_t)snprintf(sy->log + sy->log_len, sy->log_cap - sy->log_len,
+                                          "Processor %d: instr type=%c, address=0x%02X, value=%hhu\n",
+                                          tid, type, address, value);
+
+    uint8_t procNodeAddr = (address >> 4) & 0x0F;
+    uint8_t memBlockAddr = address & 0x0F;
+    uint8_t cacheIndex = memBlockAddr % sy->CS;
+    oline *L = &nd->cache[cacheIndex];
+    int hit = L->address == address ? (L->state == INVALID ? 0 : 1) : 0; /* ref :662-664 */
+    omsg m = {0};
+    if (type == 'R') {
+        if (!hit) {
+            m.type = READ_REQUEST;
+            m.sender = (uint8_t)tid;
+            m.address = address;
+            send_message(nd, procNodeAddr, m);
+            nd->waiting = 1;
+        }
+    } else {
+        if (hit) {
+            if (L->state == MODIFIED || L->state == EXCLUSIVE) {
+                L->value = value;
+                L->state = MODIFIED;
+            } else {
+                m.type = UPGRADE;
+                m.sender = (uint8_t)tid;
+                m.address = address;
+                m.value = value;
+                send_message(nd, procNodeAddr, m);
+                nd->waiting = 1;
+            }
+        } else {
+            m.type = WRITE_REQUEST;
+            m.sender = (uint8_t)tid;
+            m.address = address;
+            m.value = value;
+            send_message(nd, procNodeAddr, m);
+            nd->waiting = 1;
+        }
+    }
+}
+
+/* initializeProcessor's state part (ref :806-821) */
+static void init_node(onode *nd, int tid, int CS) {
+    for (int i = 0; i < ORC_MEM_SIZE; i++) {
+        nd->memory[i] = (uint8_t)(20 * tid + i);
+        nd->bitVector[i] = 0;
+        nd->dirState[i] = U;
+    }
+    for (int i = 0; i < CS; i++) {
+        nd->cache[i].address = 0xFF;
+        nd->cache[i].value = 0;
+        nd->cache[i].state = INVALID;
+    }
+    nd->head = nd->qcount = 0;
+    nd->nout = 0;
+    nd->waiting = 0;
+}
+
+static uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+
+uint64_t orc_digest_node(const orc_node_state *s, int node_id, int cache_size) {
+    uint64_t h = 0x243F6A8885A308D3ULL ^ ((uint64_t)node_id << 56);
+    for (int b = 0; b < ORC_MEM_SIZE; b++)
+        h = fmix64(h ^ ((uint64_t)s->memory[b] | ((uint64_t)s->dir_bitvector[b] << 8) |
+                        ((uint64_t)s->dir_state[b] << 16)));
+    for (int i = 0; i < cache_size; i++)
+        h = fmix64(h ^ ((uint64_t)s->cache_addr[i] | ((uint64_t)s->cache_value[i] << 8) |
+                        ((uint64_t)s->cache_state[i] << 16) | (1ULL << 24)));
+    return h;
+}
+
+int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
+                   const uint32_t *lens, orc_result *out, char *log, uint64_t log_cap) {
+    const int N = cfg->num_procs, CS = cfg->cache_size;
+    if (N < 1 || N > ORC_MAX_PROCS || CS < 1 || CS > ORC_MAX_CACHE || (CS & (CS - 1)) ||
+        cfg->ring_depth < 1 || cfg->ring_depth > MAX_RING)
+        return -1;
+    for (int t = 0; t < N; t++)
+        for (uint32_t i = 0; i < lens[t]; i++)
+            if (((trace[t * stride + i] >> 12) & 0x7) >= (unsigned)N) return -1;
+
+    osys *sy = (osys *)calloc(1, sizeof(osys));
+    if (!sy) return -1;
+    memset(out, 0, sizeof(*out));
+    sy->N = N;
+    sy->CS = CS;
+    sy->ring = cfg->ring_depth;
+    sy->res = out;
+    sy->log = log;
+    sy->log_cap = log ? log_cap : 0;
+    if (log && log_cap) log[0] = 0;
+    for (int t = 0; t < N; t++) {
+        init_node(&sy->node[t], t, CS);
+        sy->node[t].trace = trace + t * stride;
+        sy->node[t].count = lens[t];
+    }
+
+    for (;;) {
+        int active = 0;
+        for (int t = 0; t < N; t++) {
+            onode *nd = &sy->node[t];
+            if (nd->qcount > 0 || (!nd->waiting && nd->idx < nd->count)) active = 1;
+        }
+        if (!active) break;
+        if (cfg->max_rounds && out->rounds >= cfg->max_rounds) {
+            out->errors |= ORC_ERR_ROUNDCAP;
+            break;
+        }
+        out->rounds++;
+
+        /* every node steps on start-of-round state */
+        for (int t = 0; t < N; t++) {
+            onode *nd = &sy->node[t];
+            nd->nout = 0;
+            if (nd->qcount > 0) {
+                omsg m = nd->q[nd->head];
+                nd->head = (nd->head + 1) % (uint32_t)sy->ring;
+                nd->qcount--;
+                handle_message(sy, t, m);
+            } else if (!nd->waiting && nd->idx < nd->count) {
+                issue_instruction(sy, t);
+            }
+        }
+        /* end-of-round delivery: ascending sender, program order (sendMessage ref :741-765) */
+        for (int s = 0; s < N; s++) {
+            onode *src = &sy->node[s];
+            for (int k = 0; k < src->nout; k++) {
+                int rcv = src->out_to[k];
+                if (rcv < 0 || rcv >= N) {
+                    out->errors |= ORC_ERR_OOB;
+                    out->dropped++;
+                    continue;
+                }
+                onode *dst = &sy->node[rcv];
+                if (dst->qcount < (uint32_t)sy->ring) {
+                    dst->q[(dst->head + dst->qcount) % (uint32_t)sy->ring] = src->out[k];
+                    dst->qcount++;
+                } else {
+                    out->errors |= ORC_ERR_OVERFLOW;
+                    out->dropped++;
+                }
+            }
+        }
+        for (int t = 0; t < N; t++)
+            if (sy->node[t].qcount > out->max_depth) out->max_depth = sy->node[t].qcount;
+    }
+
+    uint64_t d = 0x9E3779B97F4A7C15ULL;
+    for (int t = 0; t < N; t++) {
+        onode *nd = &sy->node[t];
+        if (nd->waiting && !(out->errors & ORC_ERR_ROUNDCAP)) out->errors |= ORC_ERR_DEADLOCK;
+        orc_node_state *st = &out->node[t];
+        for (int b = 0; b < ORC_MEM_SIZE; b++) {
+            st->memory[b] = nd->memory[b];
+            st->dir_bitvector[b] = nd->bitVector[b];
+            st->dir_state[b] = nd->dirState[b];
+        }
+        for (int i = 0; i < CS; i++) {
+            st->cache_addr[i] = nd->cache[i].address;
+            st->cache_value[i] = nd->cache[i].value;
+            st->cache_state[i] = nd->cache[i].state;
+        }
+        d = fmix64(d ^ orc_digest_node(st, t, CS));
+    }
+    out->digest = d;
+    free(sy);
+    return 0;
+}
+
+/* ---- synthetic traces (spec shared with the device generator) ---- */
+
+uint16_t orc_gen_instr(const orc_gen *g, uint64_t sys, uint32_t node, uint32_t i) {
+    const uint64_t N = g->num_procs;
+    uint64_t key = fmix64(g->seed ^ (sys * 0x9E3779B97F4A7C15ULL + 0x632BE59BD9B4E019ULL));
+    uint64_t r = fmix64(key ^ (((uint64_t)node << 32) | i) ^ 0x8CB92BA72F3D8DD7ULL);
+    uint32_t value = (uint32_t)(r & 0xFF);
+    uint32_t blk = (uint32_t)((r >> 8) & 0xF);
+    uint32_t is_w = (uint32_t)((r >> 12) & 1);
+    uint32_t c16 = (uint32_t)((r >> 16) & 0xFFFF);
+    uint64_t u32 = r >> 32;
+    uint32_t nd = (uint32_t)((u32 * N) >> 32);
+    if (g->kind == 1) {
+        if (c16 < 58982u) { /* 90 %: WR to one of 0x00..0x03 (homed on node 0) */
+            is_w = 1;
+            nd = 0;
+            blk &= 3;
+        }
+    } else if (g->kind == 2) {
+        if (c16 < g->locality || N == 1)
+            nd = node;
+        else
+            nd = (uint32_t)((node + 1 + ((u32 * (N - 1)) >> 32)) % N);
+    }
+    if (!is_w) value = 0; /* RD carries value 0 (ref :839) */
+    return (uint16_t)((is_w << 15) | (((nd << 4) | blk) << 8) | value);
+}
+
+void orc_gen_system(const orc_gen *g, uint64_t sys, uint16_t *trace, uint64_t stride) {
+    for (uint32_t t = 0; t < g->num_procs; t++)
+        for (uint32_t i = 0; i < g->len; i++)
+            trace[t * stride + i] = orc_gen_instr(g, sys, t, i);
+}
+
+double orc_run_batch(const orc_cfg *cfg, const orc_gen *g, uint64_t sys_first, uint64_t count,
+                     int threads, uint64_t *digests, uint32_t *rounds, uint32_t *errors,
+                     uint64_t *hist_total, uint64_t *instr_total) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    uint64_t hist[ORC_NUM_TXN] = {0};
+    uint64_t instr = 0;
+    int nthr = threads > 0 ? threads : 1;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthr)
+#endif
+    {
+        uint16_t *tr = (uint16_t *)malloc(sizeof(uint16_t) * (size_t)g->num_procs * (g->len ? g->len : 1));
+        uint32_t lens[ORC_MAX_PROCS];
+        for (int t = 0; t < ORC_MAX_PROCS; t++) lens[t] = g->len;
+        orc_result *res = (orc_result *)malloc(sizeof(orc_result));
+        uint64_t lh[ORC_NUM_TXN] = {0};
+        uint64_t li = 0;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t k = 0; k < (int64_t)count; k++) {
+            uint64_t sys = sys_first + (uint64_t)k;
+            orc_gen_system(g, sys, tr, g->len);
+            orc_run_system(cfg, tr, g->len, lens, res, NULL, 0);
+            if (digests) digests[k] = res->digest;
+            if (rounds) rounds[k] = (uint32_t)res->rounds;
+            if (errors) errors[k] = res->errors;
+            for (int j = 0; j < ORC_NUM_TXN; j++) lh[j] += res->hist[j];
+            li += res->instructions;
+        }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+        {
+            for (int j = 0; j < ORC_NUM_TXN; j++) hist[j] += lh[j];
+            instr += li;
+        }
+        free(res);
+        free(tr);
+    }
+    (void)nthr;
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (hist_total)
+        for (int j = 0; j < ORC_NUM_TXN; j++) hist_total[j] += hist[j];
+    if (instr_total) *instr_total += instr;
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---- printProcessorState (ref :853-905), binary digits hand-formatted (no %B) ---- */
+
+int orc_dump_node(const orc_node_state *s, int id, int cache_size, char *buf, int cap) {
+    static const char *cst[] = {"MODIFIED", "EXCLUSIVE", "SHARED", "INVALID"};
+    static const char *dst[] = {"EM", "S", "U"};
+    int n = 0;
+#define P(...) n += snprintf(buf + n, (size_t)(cap > n ? cap - n : 0), __VA_ARGS__)
+    P("=======================================\n");
+    P(" Processor Node: %d\n", id);
+    P("=======================================\n\n");
+    P("-------- Memory State --------\n");
+    P("| Index | Address |   Value  |\n");
+    P("|----------------------------|\n");
+    for (int i = 0; i < ORC_MEM_SIZE; i++)
+        P("|  %3d  |  0x%02X   |  %5d   |\n", i, (id << 4) + i, s->memory[i]);
+    P("------------------------------\n\n");
+    P("------------ Directory State ---------------\n");
+    P("| Index | Address | State |    BitVector   |\n");
+    P("|------------------------------------------|\n");
+    for (int i = 0; i < ORC_MEM_SIZE; i++) {
+        char bits[9];
+        for (int k = 0; k < 8; k++) bits[k] = (char)('0' + ((s->dir_bitvector[i] >> (7 - k)) & 1));
+        bits[8] = 0;
+        P("|  %3d  |  0x%02X   |  %2s   |   0x%s   |\n", i, (id << 4) + i,
+          dst[s->dir_state[i] % 3], bits);
+    }
+    P("--------------------------------------------\n\n");
+    P("------------ Cache State ----------------\n");
+    P("| Index | Address | Value |    State    |\n");
+    P("|---------------------------------------|\n");
+    for (int i = 0; i < cache_size; i++)
+        P("|  %3d  |  0x%02X   |  %3d  |  %8s \t|\n", i, s->cache_addr[i], s->cache_value[i],
+          cst[s->cache_state[i] & 3]);
+    P("----------------------------------------\n\n");
+#undef P
+    return n;
+}

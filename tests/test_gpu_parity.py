@@ -1,0 +1,174 @@
+"""GPU parity: libdash on an MI355X vs the CPU oracle, through the C-ABI.
+
+Bar: bit-exact (integer/byte work). Compared per system: full final state of
+every node, per-type message histogram, lockstep round count, error bits and
+the 64-bit digest.
+"""
+import os
+import pathlib
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle_ctypes import GOLDEN, load_test_dir, run_batch, run_system
+import oracle_ctypes
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+TESTS = ["sample", "test_1", "test_2", "test_3", "test_4"]
+EXPECT_SET = {"sample": "sample", "test_1": "test_1", "test_2": "test_2", "test_3": "run_1",
+              "test_4": "run_1"}
+
+
+def expected_dir(test):
+    return GOLDEN / test if EXPECT_SET[test] == test else GOLDEN / test / EXPECT_SET[test]
+
+
+def random_batch(rng, nsys, N, maxlen, block_span=16, hot_frac=0.0, fixed_len=False):
+    if fixed_len:
+        lens = np.full((nsys, N), maxlen, dtype=np.uint32)
+    else:
+        lens = rng.integers(0, maxlen + 1, size=(nsys, N)).astype(np.uint32)
+    shape = (nsys, N, max(maxlen, 1))
+    is_w = rng.random(shape) < 0.5
+    node = rng.integers(0, N, size=shape)
+    blk = rng.integers(0, block_span, size=shape)
+    if hot_frac > 0:  # contention: a share of writes to 0x00..0x03
+        hot = rng.random(shape) < hot_frac
+        is_w |= hot
+        node = np.where(hot, 0, node)
+        blk = np.where(hot, blk & 3, blk)
+    val = np.where(is_w, rng.integers(0, 256, size=shape), 0)
+    packed = (is_w.astype(np.uint32) << 15) | (((node << 4) | blk).astype(np.uint32) << 8) | val
+    idx = np.arange(shape[2])[None, None, :]
+    packed = np.where(idx < lens[:, :, None], packed, 0).astype(np.uint16)
+    return packed, lens
+
+
+def state_arrays(nodes, N, CS):
+    out = []
+    for n in range(N):
+        s = nodes[n]
+        out.append((bytes(s.memory), bytes(s.dir_bitvector), bytes(s.dir_state),
+                    bytes(s.cache_addr)[:CS], bytes(s.cache_value)[:CS], bytes(s.cache_state)[:CS]))
+    return out
+
+
+def check_batch(dash, packed, lens, N, CS, max_rounds=0):
+    nsys = packed.shape[0]
+    with dash.Engine(nsys, num_procs=N, cache_size=CS, max_instr=packed.shape[2], keep_state=True,
+                     max_rounds=max_rounds) as eng:
+        eng.load_traces(packed, lens)
+        stats = eng.run()
+        dig, rnd, err = eng.read_results()
+        hist_total = np.zeros(13, dtype=np.uint64)
+        rounds_total = 0
+        for s in range(nsys):
+            res = run_system(packed[s], lens[s], num_procs=N, cache_size=CS, ring_depth=32,
+                             max_rounds=max_rounds or (1024 + 256 * packed.shape[2]))
+            gpu_nodes = eng.read_state(s)
+            assert state_arrays(gpu_nodes, N, CS) == state_arrays(res.node, N, CS), f"system {s}"
+            assert int(rnd[s]) == res.rounds, f"system {s} rounds"
+            assert int(err[s]) == res.errors, f"system {s} errors"
+            assert int(dig[s]) == res.digest, f"system {s} digest"
+            assert eng.read_hist(s).tolist() == list(res.hist), f"system {s} hist"
+            hist_total += np.array(list(res.hist), dtype=np.uint64)
+            rounds_total += res.rounds
+        assert stats["hist"] == hist_total.tolist()
+        assert stats["rounds_total"] == rounds_total
+        assert stats["systems"] == nsys
+        assert stats["instructions"] == int(lens.sum())
+    return stats
+
+
+@pytest.mark.parametrize("test", TESTS)
+def test_golden_through_simulate_dir(dash, test, tmp_path):
+    stats = dash.simulate_dir(GOLDEN / test, out_dir=tmp_path)
+    exp = expected_dir(test)
+    for n in range(4):
+        assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
+            (exp / f"core_{n}_output.txt").read_bytes(), f"{test} core_{n}"
+    assert stats["err_bits"] == 0
+
+
+def test_cli_reference_argv_contract(dash, tmp_path):
+    exe = dash.PKG / "cache_simulator"
+    (tmp_path / "tests").mkdir()
+    shutil.copytree(GOLDEN / "test_4", tmp_path / "tests" / "test_4")
+    p = subprocess.run([str(exe), "test_4"], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.splitlines() == [f"Processor {n} initialized" for n in range(4)]
+    for n in range(4):
+        assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
+            (GOLDEN / "test_4" / "run_1" / f"core_{n}_output.txt").read_bytes()
+    p = subprocess.run([str(exe)], cwd=tmp_path, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 1 and "Usage:" in p.stderr
+
+
+@pytest.mark.parametrize("N,CS", [(4, 4), (8, 4), (4, 1), (8, 2), (8, 8), (8, 16), (2, 4),
+                                  (3, 4), (5, 2), (1, 4)])
+def test_random_traces_bit_exact(dash, N, CS):
+    rng = np.random.default_rng(1000 * N + CS)
+    packed, lens = random_batch(rng, 160, N, 40)
+    check_batch(dash, packed, lens, N, CS)
+
+
+@pytest.mark.parametrize("N", [4, 8])
+def test_contention_and_small_address_space(dash, N):
+    rng = np.random.default_rng(77 + N)
+    packed, lens = random_batch(rng, 128, N, 48, block_span=4, hot_frac=0.7)
+    check_batch(dash, packed, lens, N, 4)
+
+
+def test_long_traces_window_refill(dash):
+    """Traces far longer than the 3-chunk LDS window, ragged lengths."""
+    rng = np.random.default_rng(5)
+    packed, lens = random_batch(rng, 24, 8, 777)
+    check_batch(dash, packed, lens, 8, 4)
+
+
+def test_edge_cases(dash):
+    rng = np.random.default_rng(9)
+    # empty traces, a single system, lengths not a multiple of 8
+    packed, lens = random_batch(rng, 1, 4, 13)
+    lens[0, :] = [0, 13, 1, 7]
+    check_batch(dash, packed, lens, 4, 4)
+    packed = np.zeros((3, 8, 8), np.uint16)
+    lens = np.zeros((3, 8), np.uint32)
+    stats = check_batch(dash, packed, lens, 8, 4)
+    assert stats["rounds_total"] == 0
+
+
+def test_error_paths_match_oracle(dash):
+    """Uniform random traces hit the reference's undefined behaviour (stale
+    EVICT_SHARED turns the empty 0xFF line EXCLUSIVE; evicting it targets
+    node 15). The engine and the oracle must flag and drop identically."""
+    rng = np.random.default_rng(123)
+    packed, lens = random_batch(rng, 400, 8, 64, fixed_len=True)
+    stats = check_batch(dash, packed, lens, 8, 4)
+    assert stats["err_bits"] & dash.ERR_OOB  # the path was exercised
+
+
+def test_round_cap(dash):
+    rng = np.random.default_rng(11)
+    packed, lens = random_batch(rng, 40, 4, 32, fixed_len=True)
+    check_batch(dash, packed, lens, 4, 4, max_rounds=20)
+
+
+@pytest.mark.parametrize("kind,loc", [(0, 0), (1, 0), (2, 49152), (2, 0), (2, 65536)])
+def test_device_generator_matches_host(dash, kind, loc):
+    """dash_generate (on-device, counter-based) == the oracle's host twin."""
+    N, CS, L, nsys, seed, base = 8, 4, 96, 200, 0x5EED, 12345
+    with dash.Engine(nsys, num_procs=N, cache_size=CS, max_instr=L) as eng:
+        eng.generate(seed, L, kind=kind, locality=loc, sys_base=base)
+        stats = eng.run()
+        dig, rnd, err = eng.read_results()
+    ref = run_batch(seed, base, nsys, num_procs=N, cache_size=CS, length=L, kind=kind,
+                    locality=loc, threads=4)
+    assert np.array_equal(dig, ref["digests"])
+    assert np.array_equal(rnd, ref["rounds"])
+    assert np.array_equal(err, ref["errors"])
+    assert stats["hist"] == ref["hist"].tolist()
+    assert stats["instructions"] == ref["instructions"]

@@ -1,0 +1,365 @@
+// dash_api.cpp -- C-ABI of libdash over HIP (handles, device buffers, launches).
+//
+// Replaces main()'s OpenMP plumbing in /root/reference/assignment.c:
+// omp_set_num_threads / queue + lock init (:135-144), the parallel region
+// (:149-155) and the per-thread private processorNode (:145).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "dash.h"
+#include "dash_device.h"
+
+struct dash_ctx {
+    dash_cfg cfg{};
+    uint32_t seg = 0;       // lanes per system (next pow2 of num_procs)
+    uint64_t groups = 0;    // waves (64/seg systems each)
+    uint32_t nchunks = 0;   // 8-instruction chunks per lane
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint4* d_trace = nullptr;
+    uint32_t* d_lens = nullptr;
+    uint64_t* d_digests = nullptr;
+    uint32_t* d_rounds = nullptr;
+    uint32_t* d_errors = nullptr;
+    uint32_t* d_state = nullptr;
+    uint32_t* d_hist = nullptr;
+    unsigned long long* d_stats = nullptr;
+    bool loaded = false;
+    bool ran = false;
+    char msg[256] = {0};
+};
+
+static int fail(dash_t* h, int code, const char* fmt, ...) {
+    if (h) {
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(h->msg, sizeof h->msg, fmt, ap);
+        va_end(ap);
+    }
+    return code;
+}
+
+#define HIPCHK(h, expr)                                                                  \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail((h), DASH_EDEVICE, "%s: %s", #expr, hipGetErrorString(e_));      \
+    } while (0)
+
+static uint32_t next_pow2(uint32_t n) {
+    uint32_t p = 1;
+    while (p < n) p <<= 1;
+    return p;
+}
+
+extern "C" {
+
+const char* dash_last_error(const dash_t* h) { return h ? h->msg : "null handle"; }
+
+void* dash_stream(dash_t* h) { return h ? (void*)h->stream : nullptr; }
+
+static void release(dash_t* h) {
+    if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    (void)hipFree(h->d_trace);
+    (void)hipFree(h->d_lens);
+    (void)hipFree(h->d_digests);
+    (void)hipFree(h->d_rounds);
+    (void)hipFree(h->d_errors);
+    (void)hipFree(h->d_state);
+    (void)hipFree(h->d_hist);
+    (void)hipFree(h->d_stats);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+}
+
+void dash_destroy(dash_t* h) {
+    release(h);
+    delete h;
+}
+
+int dash_create(const dash_cfg* cfg, dash_t** out) {
+    if (!cfg || !out) return DASH_EINVAL;
+    *out = nullptr;
+    const uint32_t N = cfg->num_procs, CS = cfg->cache_size;
+    if (N < 1 || N > DASH_MAX_PROCS) return DASH_EINVAL;
+    if (CS < 1 || CS > DASH_MAX_CACHE || (CS & (CS - 1))) return DASH_EINVAL;
+    if (cfg->max_instr > (1u << 24)) return DASH_EINVAL;
+    dash_t* h = new (std::nothrow) dash_ctx();
+    if (!h) return DASH_ENOMEM;
+    h->cfg = *cfg;
+    if (h->cfg.max_rounds == 0) h->cfg.max_rounds = 1024ull + 256ull * cfg->max_instr;
+    if (h->cfg.max_rounds > 0xFFFFFFFFull) h->cfg.max_rounds = 0xFFFFFFFFull;
+    h->seg = next_pow2(N);
+    const uint64_t spw = 64 / h->seg;
+    h->groups = (cfg->num_systems + spw - 1) / spw;
+    h->nchunks = (cfg->max_instr + 7) / 8;
+    int rc = DASH_OK;
+    auto chk = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == DASH_OK)
+            rc = fail(h, e == hipErrorOutOfMemory ? DASH_ENOMEM : DASH_EDEVICE, "%s: %s", what,
+                      hipGetErrorString(e));
+    };
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        delete h;
+        return DASH_EDEVICE;
+    }
+    if (cfg->device < 0 || cfg->device >= ndev) {
+        delete h;
+        return DASH_EINVAL;
+    }
+    chk(hipSetDevice(cfg->device), "hipSetDevice");
+    chk(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
+    chk(hipEventCreate(&h->ev0), "hipEventCreate");
+    chk(hipEventCreate(&h->ev1), "hipEventCreate");
+    const uint64_t nsys = cfg->num_systems;
+    const uint64_t trace_words = h->groups * (uint64_t)std::max<uint32_t>(h->nchunks, 1) * 64;
+    chk(hipMalloc(&h->d_trace, trace_words * sizeof(uint4)), "hipMalloc(trace)");
+    chk(hipMalloc(&h->d_lens, std::max<uint64_t>(nsys * N, 1) * sizeof(uint32_t)), "hipMalloc(lens)");
+    chk(hipMalloc(&h->d_digests, std::max<uint64_t>(nsys, 1) * sizeof(uint64_t)), "hipMalloc(digests)");
+    chk(hipMalloc(&h->d_rounds, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(rounds)");
+    chk(hipMalloc(&h->d_errors, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(errors)");
+    chk(hipMalloc(&h->d_stats, dash::STAT_WORDS * sizeof(unsigned long long)), "hipMalloc(stats)");
+    if (cfg->flags & DASH_KEEP_STATE) {
+        chk(hipMalloc(&h->d_state, std::max<uint64_t>(nsys * N, 1) * (16 + CS) * sizeof(uint32_t)),
+            "hipMalloc(state)");
+        chk(hipMalloc(&h->d_hist, std::max<uint64_t>(nsys * N, 1) * 13 * sizeof(uint32_t)),
+            "hipMalloc(hist)");
+    }
+    if (rc != DASH_OK) {
+        fprintf(stderr, "dash_create: %s\n", h->msg);
+        dash_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return DASH_OK;
+}
+
+int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const uint32_t* lens,
+                     uint64_t num_systems) {
+    if (!h || (!packed && num_systems) || !lens) return DASH_EINVAL;
+    const uint32_t N = h->cfg.num_procs, P = h->seg;
+    if (num_systems != h->cfg.num_systems) return fail(h, DASH_EINVAL, "num_systems mismatch");
+    for (uint64_t i = 0; i < num_systems * N; i++)
+        if (lens[i] > h->cfg.max_instr || lens[i] > stride)
+            return fail(h, DASH_EINVAL, "trace %llu longer than max_instr", (unsigned long long)i);
+    // lane-interleaved layout: [group][chunk][lane][8 x u16]
+    const uint64_t words = h->groups * (uint64_t)h->nchunks * 64;
+    std::vector<uint16_t> host(words * 8, 0);
+    for (uint64_t s = 0; s < num_systems; s++) {
+        const uint64_t g = s / (64 / P);
+        const uint32_t lane0 = (uint32_t)(s % (64 / P)) * P;
+        for (uint32_t t = 0; t < N; t++) {
+            const uint16_t* src = packed + (s * N + t) * stride;
+            for (uint32_t i = 0; i < lens[s * N + t]; i++) {
+                const uint16_t w = src[i];
+                if (((w >> 12) & 7u) >= N)
+                    return fail(h, DASH_EADDR, "system %llu node %u: address 0x%02X homed on node >= %u",
+                                (unsigned long long)s, t, (w >> 8) & 0x7F, N);
+                host[((g * h->nchunks + i / 8) * 64 + lane0 + t) * 8 + (i & 7)] = w;
+            }
+        }
+    }
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    if (words)
+        HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 16, hipMemcpyHostToDevice, h->stream));
+    if (num_systems)
+        HIPCHK(h, hipMemcpyAsync(h->d_lens, lens, num_systems * N * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->loaded = true;
+    h->ran = false;
+    return DASH_OK;
+}
+
+int dash_generate(dash_t* h, const dash_gen* g) {
+    if (!h || !g) return DASH_EINVAL;
+    if (g->len > h->cfg.max_instr) return fail(h, DASH_EINVAL, "gen len > max_instr");
+    if (g->kind > DASH_GEN_LOCALITY) return fail(h, DASH_EINVAL, "unknown generator kind");
+    dash::GenArgs a{};
+    a.trace = h->d_trace;
+    a.lens = h->d_lens;
+    a.nsys = h->cfg.num_systems;
+    a.ngroups = h->groups;
+    a.seed = g->seed;
+    a.sys_base = g->sys_base;
+    a.nchunks = h->nchunks;
+    a.num_procs = h->cfg.num_procs;
+    a.seg = h->seg;
+    a.kind = g->kind;
+    a.locality = g->locality;
+    a.len = g->len;
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    HIPCHK(h, dash::launch_gen(a, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->loaded = true;
+    h->ran = false;
+    return DASH_OK;
+}
+
+int dash_run(dash_t* h, dash_stats* stats) {
+    if (!h) return DASH_EINVAL;
+    if (!h->loaded) return fail(h, DASH_ESTATE, "no traces loaded");
+    dash::SimArgs a{};
+    a.trace = h->d_trace;
+    a.lens = h->d_lens;
+    a.nsys = h->cfg.num_systems;
+    a.nchunks = h->nchunks;
+    a.num_procs = h->cfg.num_procs;
+    a.max_rounds = (uint32_t)h->cfg.max_rounds;
+    a.digests = h->d_digests;
+    a.rounds = h->d_rounds;
+    a.errors = h->d_errors;
+    a.state = h->d_state;
+    a.hist_node = h->d_hist;
+    a.stats = h->d_stats;
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    HIPCHK(h, hipMemsetAsync(h->d_stats, 0, dash::STAT_WORDS * sizeof(unsigned long long), h->stream));
+    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+    HIPCHK(h, dash::launch_sim(a, h->seg, h->cfg.cache_size, h->groups, h->stream));
+    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    unsigned long long s[dash::STAT_WORDS];
+    HIPCHK(h, hipMemcpyAsync(s, h->d_stats, sizeof s, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    float ms = 0.f;
+    HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    h->ran = true;
+    if (stats) {
+        memset(stats, 0, sizeof *stats);
+        for (int k = 0; k < DASH_NUM_TXN; k++) stats->hist[k] = s[dash::STAT_HIST + k];
+        stats->instructions = s[dash::STAT_INSTR];
+        stats->rounds_total = s[dash::STAT_ROUNDS];
+        stats->rounds_max = s[dash::STAT_ROUNDS_MAX];
+        stats->systems = s[dash::STAT_SYSTEMS];
+        stats->err_systems = s[dash::STAT_ERRSYS];
+        stats->err_bits = s[dash::STAT_ERRBITS];
+        stats->dropped = s[dash::STAT_DROPS];
+        stats->max_depth = s[dash::STAT_MAXDEPTH];
+        stats->kernel_ms = ms;
+    }
+    return DASH_OK;
+}
+
+int dash_read_results(dash_t* h, uint64_t first, uint64_t count, uint64_t* digests,
+                      uint32_t* rounds, uint32_t* errors) {
+    if (!h) return DASH_EINVAL;
+    if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
+    if (first + count > h->cfg.num_systems || first + count < first)
+        return fail(h, DASH_EINVAL, "range out of bounds");
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    if (digests && count)
+        HIPCHK(h, hipMemcpyAsync(digests, h->d_digests + first, count * 8, hipMemcpyDeviceToHost, h->stream));
+    if (rounds && count)
+        HIPCHK(h, hipMemcpyAsync(rounds, h->d_rounds + first, count * 4, hipMemcpyDeviceToHost, h->stream));
+    if (errors && count)
+        HIPCHK(h, hipMemcpyAsync(errors, h->d_errors + first, count * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return DASH_OK;
+}
+
+int dash_read_state(dash_t* h, uint64_t sys, dash_node_state* out) {
+    if (!h || !out) return DASH_EINVAL;
+    if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
+    if (!h->d_state) return fail(h, DASH_ESTATE, "created without DASH_KEEP_STATE");
+    if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
+    const uint32_t N = h->cfg.num_procs, CS = h->cfg.cache_size, W = 16 + CS;
+    std::vector<uint32_t> w((size_t)N * W);
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    HIPCHK(h, hipMemcpyAsync(w.data(), h->d_state + sys * N * W, w.size() * 4, hipMemcpyDeviceToHost,
+                             h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (uint32_t t = 0; t < N; t++) {
+        dash_node_state* s = &out[t];
+        memset(s, 0, sizeof *s);
+        for (uint32_t b = 0; b < 16; b++) {
+            const uint32_t e = w[t * W + b];
+            s->memory[b] = (uint8_t)(e & 0xFF);
+            s->dir_bitvector[b] = (uint8_t)((e >> 8) & 0xFF);
+            s->dir_state[b] = (uint8_t)((e >> 16) & 3);
+        }
+        for (uint32_t i = 0; i < CS; i++) {
+            const uint32_t l = w[t * W + 16 + i];
+            s->cache_addr[i] = (uint8_t)(l & 0xFF);
+            s->cache_value[i] = (uint8_t)((l >> 8) & 0xFF);
+            s->cache_state[i] = (uint8_t)((l >> 16) & 3);
+        }
+    }
+    return DASH_OK;
+}
+
+int dash_read_hist(dash_t* h, uint64_t sys, uint32_t* hist) {
+    if (!h || !hist) return DASH_EINVAL;
+    if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
+    if (!h->d_hist) return fail(h, DASH_ESTATE, "created without DASH_KEEP_STATE");
+    if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
+    const uint32_t N = h->cfg.num_procs;
+    std::vector<uint32_t> w((size_t)N * 13);
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    HIPCHK(h, hipMemcpyAsync(w.data(), h->d_hist + sys * N * 13, w.size() * 4, hipMemcpyDeviceToHost,
+                             h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (int k = 0; k < 13; k++) {
+        hist[k] = 0;
+        for (uint32_t t = 0; t < N; t++) hist[k] += w[t * 13 + k];
+    }
+    return DASH_OK;
+}
+
+int dash_load_dir(dash_t* h, const char* dir, uint64_t sys) {
+    if (!h || !dir) return DASH_EINVAL;
+    if (h->cfg.num_systems != 1 || sys != 0)
+        return fail(h, DASH_EINVAL, "dash_load_dir loads a batch of one system");
+    char base[4096], path[4200];
+    int rc = dash_resolve_dir(dir, base, sizeof base);
+    const uint32_t N = h->cfg.num_procs, M = h->cfg.max_instr;
+    std::vector<uint16_t> tr((size_t)N * std::max<uint32_t>(M, 1), 0);
+    std::vector<uint32_t> lens(N, 0);
+    for (uint32_t t = 0; t < N; t++) {
+        snprintf(path, sizeof path, "%s/core_%u.txt", base, t);
+        rc = dash_parse_core_file(path, N, M, tr.data() + (size_t)t * std::max<uint32_t>(M, 1), &lens[t]);
+        if (rc != DASH_OK) return fail(h, rc, "%s: parse failed (%d)", path, rc);
+        printf("Processor %u initialized\n", t); /* ref :850 */
+    }
+    return dash_load_traces(h, tr.data(), std::max<uint32_t>(M, 1), lens.data(), 1);
+}
+
+int dash_simulate_dir(const char* dir, uint32_t num_procs, uint32_t cache_size, uint32_t max_instr,
+                      const char* out_dir, int device, dash_stats* stats) {
+    dash_cfg cfg{};
+    cfg.num_procs = num_procs;
+    cfg.cache_size = cache_size;
+    cfg.max_instr = max_instr;
+    cfg.flags = DASH_KEEP_STATE;
+    cfg.num_systems = 1;
+    cfg.device = device;
+    dash_t* h = nullptr;
+    int rc = dash_create(&cfg, &h);
+    if (rc != DASH_OK) return rc;
+    rc = dash_load_dir(h, dir, 0);
+    if (rc != DASH_OK) {
+        fprintf(stderr, "%s\n", h->msg);
+        dash_destroy(h);
+        return rc;
+    }
+    rc = dash_run(h, stats);
+    std::vector<dash_node_state> st(num_procs);
+    if (rc == DASH_OK) rc = dash_read_state(h, 0, st.data());
+    for (uint32_t t = 0; rc == DASH_OK && t < num_procs; t++) {
+        char path[4200];
+        snprintf(path, sizeof path, "%s/core_%u_output.txt", out_dir ? out_dir : ".", t);
+        rc = dash_dump_file(&st[t], t, cache_size, path);
+    }
+    if (rc != DASH_OK && h->msg[0]) fprintf(stderr, "%s\n", h->msg);
+    dash_destroy(h);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// dash_device.h -- argument blocks shared by the HIP kernels and the host API.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dash {
+
+// DASH_ERR_* of include/dash.h, restated for device code
+constexpr uint32_t DASH_ERR_OVERFLOW_D = 1u;
+constexpr uint32_t DASH_ERR_OOB_D = 2u;
+constexpr uint32_t DASH_ERR_CTZ0_D = 4u;
+constexpr uint32_t DASH_ERR_DEADLOCK_D = 8u;
+constexpr uint32_t DASH_ERR_ROUNDCAP_D = 16u;
+
+// device statistics block (u64 words)
+enum : uint32_t {
+    STAT_HIST = 0,  // 13 words
+    STAT_INSTR = 13,
+    STAT_ROUNDS = 14,
+    STAT_ROUNDS_MAX = 15,
+    STAT_SYSTEMS = 16,
+    STAT_ERRSYS = 17,
+    STAT_ERRBITS = 18,
+    STAT_DROPS = 19,
+    STAT_MAXDEPTH = 20,
+    STAT_WORDS = 32
+};
+
+struct SimArgs {
+    const uint4* trace;       // [group][chunk][64] x 16 B (8 packed instructions)
+    const uint32_t* lens;     // [sys * N + node]
+    uint64_t nsys;
+    uint32_t nchunks;
+    uint32_t num_procs;
+    uint32_t max_rounds;
+    uint32_t _pad;
+    uint64_t* digests;        // [sys]
+    uint32_t* rounds;         // [sys]
+    uint32_t* errors;         // [sys]
+    uint32_t* state;          // optional [(sys*N+node)*(16+CS)] raw LDS words
+    uint32_t* hist_node;      // optional [(sys*N+node)*13]
+    unsigned long long* stats;  // [STAT_WORDS]
+};
+
+struct GenArgs {
+    uint4* trace;
+    uint32_t* lens;
+    uint64_t nsys;
+    uint64_t ngroups;
+    uint64_t seed;
+    uint64_t sys_base;
+    uint32_t nchunks;
+    uint32_t num_procs;
+    uint32_t seg;
+    uint32_t kind;
+    uint32_t locality;
+    uint32_t len;
+};
+
+hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint64_t groups, hipStream_t s);
+hipError_t launch_gen(const GenArgs& g, hipStream_t s);
+
+}  // namespace dash

@@ -56,6 +56,25 @@ def cpu_baseline(args, seed, kind, locality, target_s):
                       f"oracle/dash_oracle.c lockstep restatement of assignment.c"}
 
 
+def shard(rank, world, per_gpu):
+    """Weak scaling: rank g owns global systems [g*M, (g+1)*M). Traces are keyed
+    by global id, so results do not depend on the GPU count."""
+    return rank * per_gpu, per_gpu
+
+
+def reduce_totals(elapsed, counters, device, world):
+    """The one collective: MAX of the timed region, SUM of the histograms
+    (RCCL over xGMI when backend is nccl; gloo in the CPU tests)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    c = torch.tensor(counters, dtype=torch.int64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), [int(x) for x in c.tolist()]
+
+
 def read_traffic(kind):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     f = ROOT / "profiles" / f"traffic_{kind}.json"
@@ -101,7 +120,8 @@ def main():
     M = args.systems
     eng = dash.Engine(M, num_procs=8, cache_size=args.cache_size, max_instr=args.len,
                       device=local_rank)
-    eng.generate(args.seed, args.len, kind=kind, locality=locality, sys_base=rank * M)
+    sys_base, M = shard(rank, world, M)
+    eng.generate(args.seed, args.len, kind=kind, locality=locality, sys_base=sys_base)
 
     def barrier():
         if world > 1:
@@ -120,16 +140,9 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
 
-    dev = torch.device("cuda", local_rank)
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    hist = torch.tensor(stats["hist"] + [stats["instructions"], stats["rounds_total"],
-                                         stats["err_systems"], stats["dropped"]],
-                        dtype=torch.int64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM)  # the one RCCL exchange
-    elapsed = float(t.item())
-    totals = hist.tolist()
+    elapsed, totals = reduce_totals(
+        elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
+                                  stats["dropped"]], torch.device("cuda", local_rank), world)
 
     instr_per_step = world * M * 8 * args.len
     value = instr_per_step * args.steps / elapsed

@@ -1,0 +1,55 @@
+"""Multi-process path on CPU (gloo, world_size 2): bench.py's sharding by
+global system id plus its single collective (MAX time, SUM histograms) give
+the same totals as one process over all systems. The per-rank engine here is
+the CPU oracle (no GPU in this container); on the GPU box the same code runs
+libdash over RCCL."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+import oracle_ctypes as oc
+
+PER_RANK, LEN, SEED = 24, 48, 0xBEEF
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    import torch
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    base, count = bench.shard(rank, world, PER_RANK)
+    r = oc.run_batch(SEED, base, count, num_procs=8, cache_size=4, length=LEN, threads=1)
+    counters = r["hist"].tolist() + [r["instructions"], int(r["rounds"].sum()),
+                                     int((r["errors"] != 0).sum()), 0]
+    elapsed, totals = bench.reduce_totals(float(rank + 1), counters, torch.device("cpu"), world)
+    out[rank] = (elapsed, totals, r["digests"].tolist())
+    dist.destroy_process_group()
+
+
+def test_two_rank_shards_reduce_to_single_run():
+    world = 2
+    port = _free_port()
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+        res = dict(out)
+    single = oc.run_batch(SEED, 0, PER_RANK * world, num_procs=8, cache_size=4, length=LEN, threads=2)
+    expect = single["hist"].tolist() + [single["instructions"], int(single["rounds"].sum()),
+                                        int((single["errors"] != 0).sum()), 0]
+    for rank in range(world):
+        elapsed, totals, _ = res[rank]
+        assert elapsed == float(world)  # MAX over ranks
+        assert totals == expect
+    digests = res[0][2] + res[1][2]
+    assert digests == single["digests"].tolist()  # results independent of the GPU count

@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "dash_device.h"
 
 namespace dash {
@@ -72,11 +74,59 @@ struct Lds {
     static_assert(WND % 4 == 0, "window must be 16-B aligned");
 };
 
+// byte k of a u64 held as two u32 halves
+__device__ __forceinline__ uint32_t byte_of(uint32_t lo, uint32_t hi, uint32_t k) {
+    return ((k < 4 ? lo : hi) >> (8 * (k & 3))) & 0xFFu;
+}
+
+// 4 bits -> low bit of 4 bytes
+__device__ __forceinline__ uint32_t spread4(uint32_t x) { return ((x & 15u) * 0x00204081u) & 0x01010101u; }
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+
+// segmented (P lanes) exclusive prefix sum and total of byte-packed counters,
+// on the VALU (DPP row shifts / quad perms / half-row mirror): no LDS traffic
+template <int P>
+__device__ __forceinline__ void seg_scan_total(uint32_t lo, uint32_t hi, uint32_t t, uint32_t& ex_lo,
+                                               uint32_t& ex_hi, uint32_t& to_lo, uint32_t& to_hi) {
+    uint32_t il = lo, ih = hi;
+    if constexpr (P >= 2) {
+        const uint32_t yl = dpp<0x111>(il), yh = dpp<0x111>(ih);  // row_shr:1
+        if (t >= 1) { il += yl; ih += yh; }
+    }
+    if constexpr (P >= 4) {
+        const uint32_t yl = dpp<0x112>(il), yh = dpp<0x112>(ih);  // row_shr:2
+        if (t >= 2) { il += yl; ih += yh; }
+    }
+    if constexpr (P >= 8) {
+        const uint32_t yl = dpp<0x114>(il), yh = dpp<0x114>(ih);  // row_shr:4
+        if (t >= 4) { il += yl; ih += yh; }
+    }
+    ex_lo = il - lo;
+    ex_hi = ih - hi;
+    uint32_t sl = lo, sh = hi;
+    if constexpr (P >= 2) { sl += dpp<0xB1>(sl); sh += dpp<0xB1>(sh); }    // quad_perm [1,0,3,2]
+    if constexpr (P >= 4) { sl += dpp<0x4E>(sl); sh += dpp<0x4E>(sh); }    // quad_perm [2,3,0,1]
+    if constexpr (P >= 8) { sl += dpp<0x141>(sl); sh += dpp<0x141>(sh); }  // row_half_mirror
+    to_lo = sl;
+    to_hi = sh;
+}
+
+// per byte: min(x, 32), x <= 127
+__device__ __forceinline__ uint32_t clamp32_bytes(uint32_t x) {
+    const uint32_t over = ((x + 0x5F5F5F5Fu) & 0x80808080u) >> 7;  // byte >= 33
+    const uint32_t m = over * 0xFFu;
+    return (x & ~m) | (0x20202020u & m);
+}
+
 template <int P, int CS>
 __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     using L = Lds<CS>;
     constexpr uint32_t SPW = 64 / P;
-    constexpr uint32_t SEGMASK = (P == 32) ? 0xFFFFFFFFu : ((1u << P) - 1u);
+    constexpr uint32_t SEGMASK = (1u << P) - 1u;
     __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS];
     uint16_t* const lds16 = reinterpret_cast<uint16_t*>(lds);
 
@@ -87,7 +137,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     const uint32_t N = a.num_procs;
     const bool live = sys < a.nsys && t < N;
     uint32_t len = live ? a.lens[sys * N + t] : 0u;
-    const uint32_t rcv_mask = (N >= 32) ? 0xFFFFFFFFu : ((1u << N) - 1u);
+    const uint32_t rcv_mask = (1u << N) - 1u;
 
     // initializeProcessor's state part (ref :808-820)
 #pragma unroll
@@ -108,20 +158,25 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     uint4 pend = make_uint4(0, 0, 0, 0);
     if (pend_idx < nch) pend = tr[pend_idx * 64];
 
-    uint32_t head = 0, count = 0, pc = 0, waiting = 0, last_val = 0;
+    // Every lane of a system carries the queue state of ALL the system's nodes,
+    // byte r = node r's count / tail (updated identically in every lane), so a
+    // sender finds its receiver's free slot without a cross-lane read.
+    uint32_t cnt_lo = 0, cnt_hi = 0, tail_lo = 0, tail_hi = 0;
+    uint32_t pc = 0, waiting = 0, last_val = 0;
     uint32_t err = 0, rounds = 0, maxd = 0, drops = 0;
     const uint32_t cap = a.max_rounds;
 
     for (uint32_t r = 0;; ++r) {
-        // ---- quiescence / round cap (start-of-round state) ----
+        // ---- quiescence / round cap on start-of-round state ----
+        uint32_t my_cnt = byte_of(cnt_lo, cnt_hi, t);
         bool can_issue = !waiting && pc < len;
-        bool lane_act = count != 0 || can_issue;
-        const uint64_t act = __ballot(lane_act);
+        const uint64_t act = __ballot(my_cnt != 0 || can_issue);
         if (act == 0) break;
         bool sys_act = ((uint32_t)(act >> seg) & SEGMASK) != 0;
         if (sys_act && rounds >= cap) {  // every lane of a system agrees (same `rounds`)
             err |= DASH_ERR_ROUNDCAP_D;
-            count = 0;
+            cnt_lo = cnt_hi = 0;
+            my_cnt = 0;
             len = pc;
             waiting = 0;
             can_issue = false;
@@ -138,263 +193,151 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
             }
         }
 
-        // ---- one step: pop one message (ref :167-177) or issue (ref :632-647) ----
-        const bool has_msg = count != 0;
+        // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
+        const bool has_msg = my_cnt != 0;
+        const uint32_t head = (byte_of(tail_lo, tail_hi, t) - my_cnt) & (RING - 1);
         const uint32_t m = lds[L::RNG + head * 64 + lane];
-        head = (head + (has_msg ? 1u : 0u)) & (RING - 1);
-        count -= has_msg ? 1u : 0u;
+        const uint32_t ins = lds16[(L::WND * 2) + (((pc >> 3) % WIN) * 64 + lane) * 8 + (pc & 7u)];
         const bool do_issue = !has_msg && can_issue;
-        const uint32_t ins =
-            lds16[(L::WND * 2) + (((pc >> 3) % WIN) * 64 + lane) * 8 + (pc & 7u)];
         pc += do_issue ? 1u : 0u;
+        const uint32_t pops = (uint32_t)(__ballot(has_msg) >> seg) & SEGMASK;
+        const uint32_t cp_lo = cnt_lo - spread4(pops), cp_hi = cnt_hi - spread4(pops >> 4);
 
         const uint32_t type = has_msg ? (m & 15u) : (do_issue ? (T_ISSUE_R + (ins >> 15)) : T_IDLE);
         const uint32_t addr = has_msg ? ((m >> 8) & 0xFFu) : ((ins >> 8) & 0x7Fu);
         const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         const uint32_t idx = b & (CS - 1);
-
         const uint32_t ent = lds[L::ENT + b * 64 + lane];
         const uint32_t line = lds[L::CAC + idx * 64 + lane];
+
         const uint32_t mem = ent & 0xFFu, bv = (ent >> 8) & 0xFFu, ds = (ent >> 16) & 3u;
         const uint32_t laddr = line & 0xFFu, lval = (line >> 8) & 0xFFu, lst = (line >> 16) & 3u;
         const uint32_t msender = (m >> 4) & 7u, mval = (m >> 16) & 0xFFu;
         const uint32_t msr = (m >> 24) & 7u, mds_s = (m >> 27) & 1u;
         const uint32_t ival = ins & 0xFFu;
         const uint32_t sbit = 1u << msender;
-        const uint32_t owner = (uint32_t)__builtin_ctz(bv | 0x100u);
+
+        // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), predicated ----
+        const bool isRR = type == T_RR, isWRQ = type == T_WRQ, isRRD = type == T_RRD;
+        const bool isRWR = type == T_RWR, isRID = type == T_RID, isINV = type == T_INV;
+        const bool isUPG = type == T_UPG, isWBINV = type == T_WBINV, isWBINT = type == T_WBINT;
+        const bool isFL = type == T_FLUSH, isFIA = type == T_FIA, isES = type == T_ES;
+        const bool isEMOD = type == T_EMOD, isIR = type == T_ISSUE_R, isIW = type == T_ISSUE_W;
+        const bool tH = t == H, tSR = t == msr;
+        const bool dsEM = ds == D_EM, dsS = ds == D_S, dsU = ds == D_U;
         const bool hit = laddr == addr && lst != ST_I;  // ref :662-664
+        const bool own_hit = isIW && hit && lst != ST_S;  // WR hit on M/E: local write (ref :706-710)
+        const uint32_t es_bv = bv & ~sbit;
+        const uint32_t es_pop = (uint32_t)__builtin_popcount(es_bv);
+        const uint32_t es_own = (uint32_t)__builtin_ctz(es_bv | 0x100u);
+        const bool esH = isES && tH;
+        const bool em_req = (isRR || isWRQ) && dsEM;
+        const bool ctz0 = em_req && bv == 0;  // ref UB (:209, :451) -> drop + flag
 
-        uint32_t nmem = mem, nbv = bv, nds = ds, nst = lst;
-        bool fill = false;
-        uint32_t fval = 0, fst = 0;
-        uint32_t evmode = 0;  // 1: evict if another valid line, 2: evict if valid (REPLY_WR)
-        bool vA = false, vB = false;
-        uint32_t dA = 0, dB = 0, wA = 0;
-        uint32_t inv = 0;
-        bool clrw = false, setw = false, ctz0 = false;
+        // directory entry + memory
+        uint32_t nbv = bv, nds = ds, nmem = mem;
+        if (isRR && dsS) nbv = bv | sbit;                       // :222
+        if ((isRR && dsU) || isWRQ || isUPG) { nbv = sbit; nds = D_EM; }  // :234-235 :456-457 :346-347
+        if (isFL && tH) { nds = D_S; nbv = bv | (1u << msr); nmem = mval; }  // :303-307
+        if (isFIA && tH) { nbv = 1u << msr; nmem = mval; }      // :517-520
+        if (esH) { nbv = es_bv; nds = es_pop == 0 ? D_U : (es_pop == 1 ? D_EM : ds); }  // :561-588
+        if (isEMOD) { nmem = mval; nbv = 0; nds = D_U; }        // :602-616
 
-        switch (type) {
-        case T_RR:  // ref :191-237
-            if (ds == D_EM) {
-                ctz0 = bv == 0;
-                vA = !ctz0;
-                dA = owner;
-                wA = mk(T_WBINT, t, addr, 0, msender, 0);
-            } else {
-                vA = true;
-                dA = msender;
-                wA = mk(T_RRD, t, addr, mem, 0, ds == D_S ? 1u : 0u);
-                nbv = (ds == D_S) ? (bv | sbit) : sbit;
-                nds = (ds == D_S) ? D_S : D_EM;
-            }
-            break;
-        case T_WRQ:  // ref :401-459
-            if (ds == D_EM) {
-                ctz0 = bv == 0;
-                vA = !ctz0;
-                dA = owner;
-                wA = mk(T_WBINV, t, addr, mval, msender, 0);
-            } else {
-                vA = true;
-                dA = msender;
-                wA = (ds == D_U) ? mk(T_RWR, t, addr, 0, 0, 0) : mk(T_RID, t, addr, bv & ~sbit, 0, 0);
-            }
-            nds = D_EM;
-            nbv = sbit;
-            break;
-        case T_RRD:  // ref :239-255
-            fill = true;
-            fval = mval;
-            fst = mds_s ? ST_S : ST_E;
-            evmode = 1;
-            clrw = true;
-            break;
-        case T_RWR:  // ref :461-474 (replacement unconditional)
-            fill = true;
-            fval = last_val;
-            fst = ST_M;
-            evmode = 2;
-            clrw = true;
-            break;
-        case T_RID:  // ref :351-387
-            inv = mval & rcv_mask;
-            fill = true;
-            fval = last_val;
-            fst = ST_M;
-            evmode = 1;
-            clrw = true;
-            break;
-        case T_INV:  // ref :389-399
-            if (laddr == addr) nst = ST_I;
-            break;
-        case T_UPG:  // ref :325-349
-            vA = true;
-            dA = msender;
-            wA = mk(T_RID, t, addr, bv & ~sbit, 0, 0);
-            nds = D_EM;
-            nbv = sbit;
-            break;
-        case T_WBINV:  // ref :476-503 (FLUSH_INVACK twice when H == sr)
-            vA = true;
-            dA = H;
-            wA = mk(T_FIA, t, addr, lval, msr, 0);
-            vB = true;
-            dB = msr;
-            nst = ST_I;
-            break;
-        case T_WBINT:  // ref :257-286
-            vA = true;
-            dA = H;
-            wA = mk(T_FLUSH, t, addr, lval, msr, 0);
-            vB = H != msr;
-            dB = msr;
-            nst = ST_S;
-            break;
-        case T_FLUSH:  // ref :288-323
-            if (t == H) {
-                nds = D_S;
-                nbv = bv | (1u << msr);
-                nmem = mval;
-            }
-            fill = t == msr;
-            fval = mval;
-            fst = ST_S;
-            evmode = 1;
-            clrw = true;
-            break;
-        case T_FIA:  // ref :505-536
-            if (t == H) {
-                nbv = 1u << msr;
-                nmem = mval;
-            }
-            fill = t == msr;
-            fval = last_val;
-            fst = ST_M;
-            evmode = 1;
-            clrw = true;
-            break;
-        case T_ES:  // ref :538-590
-            if (t != H) {
-                nst = ST_E;
-            } else {
-                nbv = bv & ~sbit;
-                const uint32_t sharers = (uint32_t)__builtin_popcount(nbv);
-                if (sharers == 0) {
-                    nds = D_U;
-                } else if (sharers == 1) {
-                    nds = D_EM;
-                    const uint32_t o = (uint32_t)__builtin_ctz(nbv);
-                    vA = o != H;
-                    dA = o;
-                    wA = mk(T_ES, t, addr, mem, 0, 0);
-                    if (o == H) nst = ST_E;
-                }
-            }
-            break;
-        case T_EMOD:  // ref :592-617
-            nmem = mval;
-            nbv = 0;
-            nds = D_U;
-            break;
-        case T_ISSUE_R:  // ref :666-687
-            vA = !hit;
-            dA = H;
-            wA = mk(T_RR, t, addr, 0, 0, 0);
-            setw = !hit;
-            last_val = 0;
-            break;
-        case T_ISSUE_W:  // ref :688-735
-            if (hit && lst != ST_S) {
-                fill = true;  // same address: value + MODIFIED, no eviction
-                fval = ival;
-                fst = ST_M;
-            } else {
-                vA = true;
-                dA = H;
-                wA = mk(hit ? T_UPG : T_WRQ, t, addr, ival, 0, 0);
-                setw = true;
-            }
-            last_val = ival;
-            break;
-        default:
-            break;
-        }
+        // cache line
+        const bool fill = isRRD || isRWR || isRID || ((isFL || isFIA) && tSR) || own_hit;
+        const uint32_t fval = (isRRD || isFL) ? mval : (isIW ? ival : last_val);
+        const uint32_t fst = isRRD ? (mds_s ? ST_S : ST_E) : (isFL ? ST_S : ST_M);
+        uint32_t nst = lst;
+        if ((isINV && laddr == addr) || isWBINV) nst = ST_I;    // :396-398 :501
+        if (isWBINT) nst = ST_S;                                // :284
+        if (isES && (!tH || (es_pop == 1 && es_own == H))) nst = ST_E;  // :558 :586
+        const uint32_t nline = fill ? (addr | (fval << 8) | (fst << 16)) : ((line & ~(3u << 16)) | (nst << 16));
+        // handleCacheReplacement of the line being refilled (:767-804); REPLY_WR unconditional (:467)
+        const bool ev = fill && lst != ST_I && (isRWR || laddr != addr);
 
-        // handleCacheReplacement (ref :767-804) of the line being refilled
-        const bool ev = fill && lst != ST_I && (evmode == 2 || (evmode == 1 && laddr != addr));
+        // first outgoing message
+        const bool vA = ((isRR || isWRQ) && !ctz0) || isUPG || isWBINV || isWBINT ||
+                        (esH && es_pop == 1 && es_own != H) || (isIR && !hit) || (isIW && !own_hit);
+        const uint32_t dA = em_req ? (uint32_t)__builtin_ctz(bv | 0x100u)
+                                   : ((isRR || isWRQ || isUPG) ? msender : (esH ? es_own : H));
+        uint32_t tA = T_RR;  // isIR
+        tA = isRR ? (dsEM ? T_WBINT : T_RRD) : tA;
+        tA = isWRQ ? (dsEM ? T_WBINV : (dsU ? T_RWR : T_RID)) : tA;
+        tA = isUPG ? T_RID : tA;
+        tA = isWBINV ? T_FIA : tA;
+        tA = isWBINT ? T_FLUSH : tA;
+        tA = isES ? T_ES : tA;
+        tA = isIW ? (hit ? T_UPG : T_WRQ) : tA;
+        const uint32_t valA = (isWBINV || isWBINT) ? lval
+                            : (isIW ? ival : ((isUPG || (isWRQ && !dsEM)) ? es_bv : (isWRQ ? mval : mem)));
+        const uint32_t srA = (isWBINV || isWBINT) ? msr : msender;
+        const uint32_t wA = mk(tA, t, addr, valA, srA, dsS ? 1u : 0u);
+        // second copy (WRITEBACK_INV always, WRITEBACK_INT when sr != home): to sr
+        const bool vB = isWBINV || (isWBINT && H != msr);
+        const uint32_t dB = msr;
+        const uint32_t inv = isRID ? (mval & rcv_mask) : 0u;  // REPLY_ID fan-out (:364-373)
+        // eviction notice
         const uint32_t dE = laddr >> 4;
         const bool vE = ev && dE < N;
-        const uint32_t wE = (lst == ST_M) ? mk(T_EMOD, t, laddr, lval, 0, 0) : mk(T_ES, t, laddr, 0, 0, 0);
-        if (ev && dE >= N) {  // ref UB: messageBuffers[15]; defined as drop + flag
-            err |= DASH_ERR_OOB_D;
-            ++drops;
-        }
-        if (ctz0) {
-            err |= DASH_ERR_CTZ0_D;
-            ++drops;
-        }
-        const uint32_t nline = fill ? (addr | (fval << 8) | (fst << 16))
-                                    : ((line & ~(3u << 16)) | (nst << 16));
-        if (has_msg || do_issue) {
-            lds[L::ENT + b * 64 + lane] = nmem | (nbv << 8) | (nds << 16);
-            lds[L::CAC + idx * 64 + lane] = nline;
-        }
+        const uint32_t wE = mk(lst == ST_M ? T_EMOD : T_ES, t, laddr, lval, 0, 0);
+
+        waiting = ((isIR && !hit) || (isIW && !own_hit)) ? 1u
+                  : ((isRRD || isRWR || isRID || isFL || isFIA) ? 0u : waiting);
+        last_val = isIR ? 0u : (isIW ? ival : last_val);
+        if (ev && dE >= N) { err |= DASH_ERR_OOB_D; ++drops; }  // ref UB: messageBuffers[15]
+        if (ctz0) { err |= DASH_ERR_CTZ0_D; ++drops; }
+
+        lds[L::ENT + b * 64 + lane] = nmem | (nbv << 8) | (nds << 16);
+        lds[L::CAC + idx * 64 + lane] = nline;
         if (has_msg)
             __hip_atomic_fetch_add(&lds[L::HST + (m & 15u) * 64 + lane], 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
-        waiting = setw ? 1u : (clrw ? 0u : waiting);
 
-        // ---- end-of-round delivery: per-receiver counts, segmented exclusive scan ----
-        const uint32_t cnt = (vA ? (1u << (4 * dA)) : 0u) + (vB ? (1u << (4 * dB)) : 0u) +
-                             spread_nibbles(inv) + (vE ? (1u << (4 * dE)) : 0u);
-        uint32_t incl = cnt;
-#pragma unroll
-        for (uint32_t d = 1; d < P; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, P);
-            if (t >= d) incl += y;
-        }
-        const uint32_t excl = incl - cnt;
-        const uint32_t rinfo = ((head + count) & (RING - 1)) | (count << 8);
+        // ---- end-of-round delivery: lowest sender first, program order within a sender ----
+        uint32_t c_lo = spread4(inv), c_hi = spread4(inv >> 4);
+        if (vA) { if (dA < 4) c_lo += 1u << (8 * dA); else c_hi += 1u << (8 * (dA - 4)); }
+        if (vB) { if (dB < 4) c_lo += 1u << (8 * dB); else c_hi += 1u << (8 * (dB - 4)); }
+        if (vE) { if (dE < 4) c_lo += 1u << (8 * dE); else c_hi += 1u << (8 * (dE - 4)); }
+        uint32_t ex_lo, ex_hi, to_lo, to_hi;
+        seg_scan_total<P>(c_lo, c_hi, t, ex_lo, ex_hi, to_lo, to_hi);
 
         auto deliver = [&](bool v, uint32_t d, uint32_t w, uint32_t local) {
-            const uint32_t ri = __shfl(rinfo, seg + d);
-            const uint32_t pos = ((excl >> (4 * d)) & 15u) + local;
-            const bool ok = (ri >> 8) + pos < RING;
-            if (v && ok) lds[L::RNG + (((ri & (RING - 1)) + pos) & (RING - 1)) * 64 + seg + d] = w;
-            if (v && !ok) {
-                err |= DASH_ERR_OVERFLOW_D;
-                ++drops;
-            }
+            const uint32_t pos = byte_of(ex_lo, ex_hi, d) + local;
+            const bool ok = byte_of(cp_lo, cp_hi, d) + pos < RING;
+            const uint32_t slot = (byte_of(tail_lo, tail_hi, d) + pos) & (RING - 1);
+            if (v && ok) lds[L::RNG + slot * 64 + seg + d] = w;
+            if (v && !ok) { err |= DASH_ERR_OVERFLOW_D; ++drops; }
         };
-        deliver(vA, dA & (P - 1), wA, 0u);
-        deliver(vB, dB & (P - 1), wA, (vA && dA == dB) ? 1u : 0u);
+        const uint32_t dA7 = dA & 7u, dE7 = dE & 7u;
+        deliver(vA, dA7, wA, 0u);
+        deliver(vB, dB, wA, (vA && dA7 == dB) ? 1u : 0u);
         uint32_t im = inv;
-        const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
-        while (__ballot(im != 0) != 0) {
-            const uint32_t j = (uint32_t)__builtin_ctz(im | 0x100u) & (P - 1);
-            deliver(im != 0, j, winv, ((vA && dA == j) ? 1u : 0u) + ((vB && dB == j) ? 1u : 0u));
-            im &= im - 1u;
+        if (__ballot(im != 0) != 0) {
+            const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
+            do {
+                const uint32_t j = (uint32_t)__builtin_ctz(im | 0x100u) & 7u;
+                deliver(im != 0, j, winv, ((vA && dA7 == j) ? 1u : 0u) + ((vB && dB == j) ? 1u : 0u));
+                im &= im - 1u;
+            } while (__ballot(im != 0) != 0);
         }
-        const uint32_t dEs = dE & (P - 1);
-        deliver(vE, dEs, wE,
-                ((vA && dA == dEs) ? 1u : 0u) + ((vB && dB == dEs) ? 1u : 0u) + ((inv >> dEs) & 1u));
+        deliver(vE, dE7, wE,
+                ((vA && dA7 == dE7) ? 1u : 0u) + ((vB && dB == dE7) ? 1u : 0u) + ((inv >> dE7) & 1u));
 
-        const uint32_t xl = __shfl(excl, seg + P - 1);
-        const uint32_t cl = __shfl(cnt, seg + P - 1);
-        const uint32_t tot = ((xl >> (4 * t)) & 15u) + ((cl >> (4 * t)) & 15u);
-        count = min(count + tot, RING);
-        maxd = max(maxd, count);
+        // every lane: new counts = min(count - pop + arrivals, RING); tails advance by delivered
+        const uint32_t n_lo = clamp32_bytes(cp_lo + to_lo), n_hi = clamp32_bytes(cp_hi + to_hi);
+        tail_lo = (tail_lo + (n_lo - cp_lo)) & 0x1F1F1F1Fu;
+        tail_hi = (tail_hi + (n_hi - cp_hi)) & 0x1F1F1F1Fu;
+        cnt_lo = n_lo;
+        cnt_hi = n_hi;
+        maxd = max(maxd, byte_of(cnt_lo, cnt_hi, t));
     }
 
     // ---- results ----
     if (waiting) err |= DASH_ERR_DEADLOCK_D;
     uint64_t h = 0x243F6A8885A308D3ull ^ ((uint64_t)t << 56);
-#pragma unroll
     for (uint32_t b = 0; b < 16; ++b) h = fmix64(h ^ (uint64_t)lds[L::ENT + b * 64 + lane]);
-#pragma unroll
-    for (uint32_t i = 0; i < CS; ++i)
-        h = fmix64(h ^ ((uint64_t)lds[L::CAC + i * 64 + lane] | (1ull << 24)));
+    for (uint32_t i = 0; i < CS; ++i) h = fmix64(h ^ ((uint64_t)lds[L::CAC + i * 64 + lane] | (1ull << 24)));
     uint64_t dg = 0x9E3779B97F4A7C15ull;
     uint32_t serr = err;
 #pragma unroll
@@ -403,43 +346,39 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         if (n < N) dg = fmix64(dg ^ hn);
         serr |= __shfl(err, seg + n);
     }
-    const uint64_t gsys = sys;
     if (live && t == 0) {
-        a.digests[gsys] = dg;
-        a.rounds[gsys] = rounds;
-        a.errors[gsys] = serr;
+        a.digests[sys] = dg;
+        a.rounds[sys] = rounds;
+        a.errors[sys] = serr;
     }
     if (a.state && live) {
-        uint32_t* st = a.state + (gsys * N + t) * (16 + CS);
-#pragma unroll
+        uint32_t* st = a.state + (sys * N + t) * (16 + CS);
         for (uint32_t b = 0; b < 16; ++b) st[b] = lds[L::ENT + b * 64 + lane];
-#pragma unroll
         for (uint32_t i = 0; i < CS; ++i) st[16 + i] = lds[L::CAC + i * 64 + lane];
     }
     if (a.hist_node && live) {
-        uint32_t* hs = a.hist_node + (gsys * N + t) * 13;
-#pragma unroll
+        uint32_t* hs = a.hist_node + (sys * N + t) * 13;
         for (uint32_t k = 0; k < 13; ++k) hs[k] = lds[L::HST + k * 64 + lane];
     }
 
-    // ---- global statistics: one wave reduction, then one atomic per counter ----
+    // ---- global statistics: wave reductions, one atomic per counter per wave ----
+    const bool head_lane = live && t == 0;
+    unsigned long long* S = a.stats;
     auto wsum = [](uint64_t v) {
-#pragma unroll
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         return v;
     };
     auto wmax = [](uint64_t v) {
-#pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             const uint64_t u = __shfl_xor(v, o);
             v = u > v ? u : v;
         }
         return v;
     };
-    uint64_t hsum[13];
-#pragma unroll
-    for (uint32_t k = 0; k < 13; ++k) hsum[k] = wsum(live ? lds[L::HST + k * 64 + lane] : 0u);
-    const bool head_lane = live && t == 0;
+    for (uint32_t k = 0; k < 13; ++k) {
+        const uint64_t v = wsum(live ? lds[L::HST + k * 64 + lane] : 0u);
+        if (lane == 0 && v) atomicAdd(&S[STAT_HIST + k], (unsigned long long)v);
+    }
     const uint64_t s_instr = wsum(live ? pc : 0u);
     const uint64_t s_rounds = wsum(head_lane ? rounds : 0u);
     const uint64_t m_rounds = wmax(head_lane ? rounds : 0u);
@@ -448,13 +387,8 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     const uint64_t s_drops = wsum(live ? drops : 0u);
     const uint64_t m_depth = wmax(live ? maxd : 0u);
     uint64_t ebits = live ? err : 0u;
-#pragma unroll
     for (int o = 32; o > 0; o >>= 1) ebits |= __shfl_xor(ebits, o);
     if (lane == 0) {
-        unsigned long long* S = a.stats;
-#pragma unroll
-        for (uint32_t k = 0; k < 13; ++k)
-            if (hsum[k]) atomicAdd(&S[STAT_HIST + k], (unsigned long long)hsum[k]);
         atomicAdd(&S[STAT_INSTR], (unsigned long long)s_instr);
         atomicAdd(&S[STAT_ROUNDS], (unsigned long long)s_rounds);
         atomicMax(&S[STAT_ROUNDS_MAX], (unsigned long long)m_rounds);
@@ -468,51 +402,53 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
 
 // ---- synthetic trace generator (spec: DESIGN.md §gen; host twin in oracle/) ----
 __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t total = g.ngroups * g.nchunks * 64ull;
-    if (gid >= total) return;
-    const uint32_t lane = (uint32_t)(gid & 63u);
-    const uint64_t rest = gid >> 6;
-    const uint32_t chunk = (uint32_t)(rest % g.nchunks);
-    const uint64_t group = rest / g.nchunks;
     const uint32_t P = g.seg;
-    const uint32_t t = lane % P;
-    const uint64_t sys = group * (64u / P) + lane / P;
-    const bool live = sys < g.nsys && t < g.num_procs;
-    uint32_t w[4] = {0, 0, 0, 0};
-    if (live) {
-        const uint64_t N = g.num_procs;
-        const uint64_t key = fmix64(g.seed ^ ((g.sys_base + sys) * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
+    const uint64_t N = g.num_procs;
+    for (uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
+         gid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t lane = (uint32_t)(gid & 63u);
+        const uint64_t rest = gid >> 6;
+        const uint32_t chunk = (uint32_t)(rest % g.nchunks);
+        const uint64_t group = rest / g.nchunks;
+        const uint32_t t = lane % P;
+        const uint64_t sys = group * (64u / P) + lane / P;
+        const bool live = sys < g.nsys && t < g.num_procs;
+        uint32_t w[4] = {0, 0, 0, 0};
+        if (live) {
+            const uint64_t key =
+                fmix64(g.seed ^ ((g.sys_base + sys) * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t i = chunk * 8 + k;
-            if (i >= g.len) break;
-            const uint64_t r = fmix64(key ^ (((uint64_t)t << 32) | i) ^ 0x8CB92BA72F3D8DD7ull);
-            uint32_t value = (uint32_t)(r & 0xFF);
-            uint32_t blk = (uint32_t)((r >> 8) & 0xF);
-            uint32_t is_w = (uint32_t)((r >> 12) & 1);
-            const uint32_t c16 = (uint32_t)((r >> 16) & 0xFFFF);
-            const uint64_t u32 = r >> 32;
-            uint32_t nd = (uint32_t)((u32 * N) >> 32);
-            if (g.kind == 1u) {
-                if (c16 < 58982u) {
-                    is_w = 1;
-                    nd = 0;
-                    blk &= 3u;
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t i = chunk * 8 + k;
+                if (i >= g.len) break;
+                const uint64_t r = fmix64(key ^ (((uint64_t)t << 32) | i) ^ 0x8CB92BA72F3D8DD7ull);
+                uint32_t value = (uint32_t)(r & 0xFF);
+                uint32_t blk = (uint32_t)((r >> 8) & 0xF);
+                uint32_t is_w = (uint32_t)((r >> 12) & 1);
+                const uint32_t c16 = (uint32_t)((r >> 16) & 0xFFFF);
+                const uint64_t u32 = r >> 32;
+                uint32_t nd = (uint32_t)((u32 * N) >> 32);
+                if (g.kind == 1u) {  // contention: 90 % WR to 0x00..0x03
+                    if (c16 < 58982u) {
+                        is_w = 1;
+                        nd = 0;
+                        blk &= 3u;
+                    }
+                } else if (g.kind == 2u) {  // locality
+                    if (c16 < g.locality || N == 1)
+                        nd = t;
+                    else
+                        nd = (uint32_t)((t + 1 + ((u32 * (N - 1)) >> 32)) % N);
                 }
-            } else if (g.kind == 2u) {
-                if (c16 < g.locality || N == 1)
-                    nd = t;
-                else
-                    nd = (uint32_t)((t + 1 + ((u32 * (N - 1)) >> 32)) % N);
+                if (!is_w) value = 0;  // RD carries value 0 (ref :839)
+                const uint32_t rec = (is_w << 15) | (((nd << 4) | blk) << 8) | value;
+                w[k >> 1] |= rec << (16 * (k & 1));
             }
-            if (!is_w) value = 0;
-            const uint32_t rec = (is_w << 15) | (((nd << 4) | blk) << 8) | value;
-            w[k >> 1] |= rec << (16 * (k & 1));
+            if (chunk == 0) g.lens[sys * g.num_procs + t] = g.len;
         }
-        if (chunk == 0) g.lens[sys * g.num_procs + t] = g.len;
+        g.trace[gid] = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    g.trace[gid] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 template <int P, int CS>
@@ -547,7 +483,7 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint64_t grou
 hipError_t launch_gen(const GenArgs& g, hipStream_t s) {
     const uint64_t total = g.ngroups * g.nchunks * 64ull;
     if (total == 0) return hipSuccess;
-    const uint64_t blocks = (total + 255) / 256;
+    const uint64_t blocks = std::min<uint64_t>((total + 255) / 256, 256ull * 64);  // grid-stride
     hipLaunchKernelGGL(gen_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, g);
     return hipGetLastError();
 }

@@ -34,6 +34,15 @@ enum : uint32_t {
 enum : uint32_t { ST_M = 0, ST_E = 1, ST_S = 2, ST_I = 3 };  // cacheLineState (ref :17)
 enum : uint32_t { D_EM = 0, D_S = 1, D_U = 2 };              // directoryEntryState (ref :28)
 
+#define B(x) (1u << (x))
+constexpr uint32_t M_CLRW = B(T_RRD) | B(T_RWR) | B(T_RID) | B(T_FLUSH) | B(T_FIA);
+// default outgoing type per handled type (nibble per type): UPGRADE->REPLY_ID,
+// WRITEBACK_INV->FLUSH_INVACK, WRITEBACK_INT->FLUSH, EVICT_SHARED->EVICT_SHARED,
+// RD miss->READ_REQUEST, WR miss->WRITE_REQUEST; READ/WRITE_REQUEST resolved by dir state
+constexpr uint64_t TA_BASE = ((uint64_t)T_RID << (4 * T_UPG)) | ((uint64_t)T_FIA << (4 * T_WBINV)) |
+                             ((uint64_t)T_FLUSH << (4 * T_WBINT)) | ((uint64_t)T_ES << (4 * T_ES)) |
+                             ((uint64_t)T_RR << (4 * T_ISSUE_R)) | ((uint64_t)T_WRQ << (4 * T_ISSUE_W));
+
 constexpr uint32_t RING = 32;    // per-node queue depth (ref MSG_BUFFER_SIZE 256)
 constexpr uint32_t WIN = 3;      // trace window chunks per lane
 constexpr uint32_t PERIOD = 8;   // window refill period in rounds (= chunk length)
@@ -218,75 +227,84 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         const uint32_t ival = ins & 0xFFu;
         const uint32_t sbit = 1u << msender;
 
-        // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), predicated ----
-        const bool isRR = type == T_RR, isWRQ = type == T_WRQ, isRRD = type == T_RRD;
-        const bool isRWR = type == T_RWR, isRID = type == T_RID, isINV = type == T_INV;
-        const bool isUPG = type == T_UPG, isWBINV = type == T_WBINV, isWBINT = type == T_WBINT;
-        const bool isFL = type == T_FLUSH, isFIA = type == T_FIA, isES = type == T_ES;
-        const bool isEMOD = type == T_EMOD, isIR = type == T_ISSUE_R, isIW = type == T_ISSUE_W;
+        // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
+        // one-hot type; every predicate below is bitwise so the step stays branch-free
+        const uint32_t tb = 1u << type;
+        auto any = [&](uint32_t mask) { return (tb & mask) != 0u; };
         const bool tH = t == H, tSR = t == msr;
         const bool dsEM = ds == D_EM, dsS = ds == D_S, dsU = ds == D_U;
-        const bool hit = laddr == addr && lst != ST_I;  // ref :662-664
-        const bool own_hit = isIW && hit && lst != ST_S;  // WR hit on M/E: local write (ref :706-710)
-        const uint32_t es_bv = bv & ~sbit;
+        const bool same = laddr == addr;
+        const bool hit = same & (lst != ST_I);              // ref :662-664
+        const bool own_hit = any(B(T_ISSUE_W)) & hit & (lst != ST_S);  // WR hit on M/E (:706-710)
+        const uint32_t es_bv = bv & ~sbit;                  // also UPGRADE/WRITE_REQUEST's sharer list
         const uint32_t es_pop = (uint32_t)__builtin_popcount(es_bv);
         const uint32_t es_own = (uint32_t)__builtin_ctz(es_bv | 0x100u);
-        const bool esH = isES && tH;
-        const bool em_req = (isRR || isWRQ) && dsEM;
-        const bool ctz0 = em_req && bv == 0;  // ref UB (:209, :451) -> drop + flag
+        const bool esH = any(B(T_ES)) & tH;
+        const bool es_one = esH & (es_pop == 1u);
+        const bool em_req = any(B(T_RR) | B(T_WRQ)) & dsEM;
+        const bool ctz0 = em_req & (bv == 0u);              // ref UB (:209, :451): drop + flag
+        const bool homeH = tH & any(B(T_FLUSH) | B(T_FIA));
 
         // directory entry + memory
-        uint32_t nbv = bv, nds = ds, nmem = mem;
-        if (isRR && dsS) nbv = bv | sbit;                       // :222
-        if ((isRR && dsU) || isWRQ || isUPG) { nbv = sbit; nds = D_EM; }  // :234-235 :456-457 :346-347
-        if (isFL && tH) { nds = D_S; nbv = bv | (1u << msr); nmem = mval; }  // :303-307
-        if (isFIA && tH) { nbv = 1u << msr; nmem = mval; }      // :517-520
-        if (esH) { nbv = es_bv; nds = es_pop == 0 ? D_U : (es_pop == 1 ? D_EM : ds); }  // :561-588
-        if (isEMOD) { nmem = mval; nbv = 0; nds = D_U; }        // :602-616
+        const bool to_req = (any(B(T_RR)) & dsU) | any(B(T_WRQ) | B(T_UPG));  // :234 :456 :346
+        uint32_t nbv = (any(B(T_RR)) & dsS) ? (bv | sbit) : bv;                // :222
+        nbv = to_req ? sbit : nbv;
+        nbv = homeH ? ((any(B(T_FLUSH)) ? bv : 0u) | (1u << msr)) : nbv;       // :304 :517
+        nbv = esH ? es_bv : nbv;                                               // :561
+        nbv = any(B(T_EMOD)) ? 0u : nbv;                                       // :615
+        uint32_t nds = to_req ? (uint32_t)D_EM : ds;
+        nds = (homeH & any(B(T_FLUSH))) ? (uint32_t)D_S : nds;                  // :303
+        nds = esH ? (es_pop == 0u ? (uint32_t)D_U : (es_pop == 1u ? (uint32_t)D_EM : ds)) : nds;
+        nds = any(B(T_EMOD)) ? (uint32_t)D_U : nds;                             // :616
+        const uint32_t nmem = (homeH | any(B(T_EMOD))) ? mval : mem;           // :307 :520 :602
 
         // cache line
-        const bool fill = isRRD || isRWR || isRID || ((isFL || isFIA) && tSR) || own_hit;
-        const uint32_t fval = (isRRD || isFL) ? mval : (isIW ? ival : last_val);
-        const uint32_t fst = isRRD ? (mds_s ? ST_S : ST_E) : (isFL ? ST_S : ST_M);
-        uint32_t nst = lst;
-        if ((isINV && laddr == addr) || isWBINV) nst = ST_I;    // :396-398 :501
-        if (isWBINT) nst = ST_S;                                // :284
-        if (isES && (!tH || (es_pop == 1 && es_own == H))) nst = ST_E;  // :558 :586
+        const bool fill = any(B(T_RRD) | B(T_RWR) | B(T_RID)) | (any(B(T_FLUSH) | B(T_FIA)) & tSR) | own_hit;
+        const uint32_t fval = any(B(T_RRD) | B(T_FLUSH)) ? mval : (any(B(T_ISSUE_W)) ? ival : last_val);
+        const uint32_t fst = any(B(T_RRD)) ? (mds_s ? ST_S : ST_E) : (any(B(T_FLUSH)) ? ST_S : ST_M);
+        uint32_t nst = ((any(B(T_INV)) & same) | any(B(T_WBINV))) ? ST_I : lst;  // :396-398 :501
+        nst = any(B(T_WBINT)) ? ST_S : nst;                                    // :284
+        nst = (any(B(T_ES)) & (!tH | (es_one & (es_own == H)))) ? ST_E : nst;  // :558 :586
         const uint32_t nline = fill ? (addr | (fval << 8) | (fst << 16)) : ((line & ~(3u << 16)) | (nst << 16));
-        // handleCacheReplacement of the line being refilled (:767-804); REPLY_WR unconditional (:467)
-        const bool ev = fill && lst != ST_I && (isRWR || laddr != addr);
+        // handleCacheReplacement of the refilled line (:767-804); REPLY_WR unconditional (:467)
+        const bool ev = fill & (lst != ST_I) & (any(B(T_RWR)) | !same);
 
-        // first outgoing message
-        const bool vA = ((isRR || isWRQ) && !ctz0) || isUPG || isWBINV || isWBINT ||
-                        (esH && es_pop == 1 && es_own != H) || (isIR && !hit) || (isIW && !own_hit);
-        const uint32_t dA = em_req ? (uint32_t)__builtin_ctz(bv | 0x100u)
-                                   : ((isRR || isWRQ || isUPG) ? msender : (esH ? es_own : H));
-        uint32_t tA = T_RR;  // isIR
-        tA = isRR ? (dsEM ? T_WBINT : T_RRD) : tA;
-        tA = isWRQ ? (dsEM ? T_WBINV : (dsU ? T_RWR : T_RID)) : tA;
-        tA = isUPG ? T_RID : tA;
-        tA = isWBINV ? T_FIA : tA;
-        tA = isWBINT ? T_FLUSH : tA;
-        tA = isES ? T_ES : tA;
-        tA = isIW ? (hit ? T_UPG : T_WRQ) : tA;
-        const uint32_t valA = (isWBINV || isWBINT) ? lval
-                            : (isIW ? ival : ((isUPG || (isWRQ && !dsEM)) ? es_bv : (isWRQ ? mval : mem)));
-        const uint32_t srA = (isWBINV || isWBINT) ? msr : msender;
+        // primary outgoing message: the handler's reply/forward, or else the eviction
+        // notice -- no handler sends both (fills never reply), so one slot serves both
+        const bool vA = (any(B(T_RR) | B(T_WRQ)) & !ctz0) | any(B(T_UPG) | B(T_WBINV) | B(T_WBINT)) |
+                        (es_one & (es_own != H)) | (any(B(T_ISSUE_R) | B(T_ISSUE_W)) & !hit) |
+                        (any(B(T_ISSUE_W)) & hit & !own_hit);
+        uint32_t dA = any(B(T_RR) | B(T_WRQ) | B(T_UPG)) ? msender : H;
+        dA = em_req ? (uint32_t)__builtin_ctz(bv | 0x100u) : dA;
+        dA = esH ? es_own : dA;
+        // reply type per request type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453)
+        uint32_t tA = (uint32_t)((TA_BASE >> (4 * type)) & 15u);
+        tA = any(B(T_RR)) ? (dsEM ? T_WBINT : T_RRD) : tA;
+        tA = any(B(T_WRQ)) ? (dsEM ? T_WBINV : (dsU ? T_RWR : T_RID)) : tA;
+        tA = (any(B(T_ISSUE_W)) & hit) ? T_UPG : tA;
+        uint32_t valA = any(B(T_WBINV) | B(T_WBINT)) ? lval : mem;
+        valA = any(B(T_ISSUE_W)) ? ival : valA;
+        valA = (any(B(T_UPG)) | (any(B(T_WRQ)) & !dsEM)) ? es_bv : valA;
+        valA = (any(B(T_WRQ)) & dsEM) ? mval : valA;
+        const uint32_t srA = any(B(T_WBINV) | B(T_WBINT)) ? msr : msender;
         const uint32_t wA = mk(tA, t, addr, valA, srA, dsS ? 1u : 0u);
-        // second copy (WRITEBACK_INV always, WRITEBACK_INT when sr != home): to sr
-        const bool vB = isWBINV || (isWBINT && H != msr);
-        const uint32_t dB = msr;
-        const uint32_t inv = isRID ? (mval & rcv_mask) : 0u;  // REPLY_ID fan-out (:364-373)
-        // eviction notice
         const uint32_t dE = laddr >> 4;
-        const bool vE = ev && dE < N;
+        const bool vE = ev & (dE < N);
         const uint32_t wE = mk(lst == ST_M ? T_EMOD : T_ES, t, laddr, lval, 0, 0);
+        const bool vP = vA | vE;
+        const uint32_t dP = (vA ? dA : dE) & 7u;
+        const uint32_t wP = vA ? wA : wE;
+        // second copy of a flush: WRITEBACK_INV always (:498), WRITEBACK_INT if sr != home (:281)
+        const bool vB = any(B(T_WBINV)) | (any(B(T_WBINT)) & (H != msr));
+        const uint32_t dB = msr;
+        const uint32_t inv = any(B(T_RID)) ? (mval & rcv_mask) : 0u;  // REPLY_ID fan-out (:364-373)
 
-        waiting = ((isIR && !hit) || (isIW && !own_hit)) ? 1u
-                  : ((isRRD || isRWR || isRID || isFL || isFIA) ? 0u : waiting);
-        last_val = isIR ? 0u : (isIW ? ival : last_val);
-        if (ev && dE >= N) { err |= DASH_ERR_OOB_D; ++drops; }  // ref UB: messageBuffers[15]
-        if (ctz0) { err |= DASH_ERR_CTZ0_D; ++drops; }
+        waiting = (any(B(T_ISSUE_R) | B(T_ISSUE_W)) & !own_hit & !(any(B(T_ISSUE_R)) & hit))
+                      ? 1u : (any(M_CLRW) ? 0u : waiting);
+        last_val = any(B(T_ISSUE_R)) ? 0u : (any(B(T_ISSUE_W)) ? ival : last_val);
+        const bool oob = ev & (dE >= N);  // ref UB: messageBuffers[15] -> drop + flag
+        err |= (oob ? DASH_ERR_OOB_D : 0u) | (ctz0 ? DASH_ERR_CTZ0_D : 0u);
+        drops += (oob ? 1u : 0u) + (ctz0 ? 1u : 0u);
 
         lds[L::ENT + b * 64 + lane] = nmem | (nbv << 8) | (nds << 16);
         lds[L::CAC + idx * 64 + lane] = nline;
@@ -295,34 +313,40 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
 
         // ---- end-of-round delivery: lowest sender first, program order within a sender ----
+        // per-receiver byte counts of this lane's sends, segmented exclusive scan + total
         uint32_t c_lo = spread4(inv), c_hi = spread4(inv >> 4);
-        if (vA) { if (dA < 4) c_lo += 1u << (8 * dA); else c_hi += 1u << (8 * (dA - 4)); }
-        if (vB) { if (dB < 4) c_lo += 1u << (8 * dB); else c_hi += 1u << (8 * (dB - 4)); }
-        if (vE) { if (dE < 4) c_lo += 1u << (8 * dE); else c_hi += 1u << (8 * (dE - 4)); }
+        const uint32_t oneP = vP ? (1u << (8 * (dP & 3u))) : 0u;
+        const uint32_t oneB = vB ? (1u << (8 * (dB & 3u))) : 0u;
+        c_lo += (dP < 4u ? oneP : 0u) + (dB < 4u ? oneB : 0u);
+        c_hi += (dP < 4u ? 0u : oneP) + (dB < 4u ? 0u : oneB);
         uint32_t ex_lo, ex_hi, to_lo, to_hi;
         seg_scan_total<P>(c_lo, c_hi, t, ex_lo, ex_hi, to_lo, to_hi);
+        // free-slot cursor and fill level per receiver (bytes): tail + excl, count-after-pop + excl
+        const uint32_t sl_lo = tail_lo + ex_lo, sl_hi = tail_hi + ex_hi;
+        const uint32_t fl_lo = cp_lo + ex_lo, fl_hi = cp_hi + ex_hi;
 
         auto deliver = [&](bool v, uint32_t d, uint32_t w, uint32_t local) {
-            const uint32_t pos = byte_of(ex_lo, ex_hi, d) + local;
-            const bool ok = byte_of(cp_lo, cp_hi, d) + pos < RING;
-            const uint32_t slot = (byte_of(tail_lo, tail_hi, d) + pos) & (RING - 1);
-            if (v && ok) lds[L::RNG + slot * 64 + seg + d] = w;
-            if (v && !ok) { err |= DASH_ERR_OVERFLOW_D; ++drops; }
+            const uint32_t sh = 8u * (d & 3u);
+            const bool hi = d >= 4u;
+            const uint32_t fill_d = ((hi ? fl_hi : fl_lo) >> sh) & 0xFFu;
+            const uint32_t slot = ((((hi ? sl_hi : sl_lo) >> sh) & 0xFFu) + local) & (RING - 1);
+            const bool ok = fill_d + local < RING;
+            if (v & ok) lds[L::RNG + slot * 64 + seg + d] = w;
+            const bool dropped = v & !ok;
+            err |= dropped ? DASH_ERR_OVERFLOW_D : 0u;
+            drops += dropped ? 1u : 0u;
         };
-        const uint32_t dA7 = dA & 7u, dE7 = dE & 7u;
-        deliver(vA, dA7, wA, 0u);
-        deliver(vB, dB, wA, (vA && dA7 == dB) ? 1u : 0u);
         uint32_t im = inv;
-        if (__ballot(im != 0) != 0) {
+        if (__ballot(im != 0) != 0) {  // INVs precede the eviction notice (ref :364-379)
             const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
             do {
                 const uint32_t j = (uint32_t)__builtin_ctz(im | 0x100u) & 7u;
-                deliver(im != 0, j, winv, ((vA && dA7 == j) ? 1u : 0u) + ((vB && dB == j) ? 1u : 0u));
+                deliver(im != 0, j, winv, 0u);
                 im &= im - 1u;
             } while (__ballot(im != 0) != 0);
         }
-        deliver(vE, dE7, wE,
-                ((vA && dA7 == dE7) ? 1u : 0u) + ((vB && dB == dE7) ? 1u : 0u) + ((inv >> dE7) & 1u));
+        deliver(vP, dP, wP, (inv >> dP) & 1u);
+        deliver(vB, dB, wA, (vA & (dP == dB)) ? 1u : 0u);
 
         // every lane: new counts = min(count - pop + arrivals, RING); tails advance by delivered
         const uint32_t n_lo = clamp32_bytes(cp_lo + to_lo), n_hi = clamp32_bytes(cp_hi + to_hi);

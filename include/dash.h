@@ -36,7 +36,9 @@ extern "C" {
 #define DASH_MEM_SIZE 16   /* MEM_SIZE (ref :8) */
 #define DASH_MAX_PROCS 8   /* bitVector is one byte (ref :63) */
 #define DASH_MAX_CACHE 16
-#define DASH_RING_DEPTH 32 /* per-node LDS queue (ref MSG_BUFFER_SIZE 256, :9) */
+#define DASH_RING_DEPTH 256 /* per-node queue capacity = ref MSG_BUFFER_SIZE (:9); the engine
+                              runs shallower LDS queues first and re-runs, from scratch, any
+                              system that would fill one (16 -> 32 -> 256) */
 #define DASH_NUM_TXN 13    /* transactionType (ref :30-44) */
 
 /* return codes */
@@ -50,7 +52,7 @@ extern "C" {
 #define DASH_ESTATE -7   /* call out of order (e.g. read_state before run) */
 
 /* per-system protocol fault bits (reference UB made defined) */
-#define DASH_ERR_OVERFLOW 1u  /* receiver queue full: dropped (ref :754-761) */
+#define DASH_ERR_OVERFLOW 1u  /* receiver queue (256) full: dropped (ref :754-761) */
 #define DASH_ERR_OOB 2u       /* receiver >= N: dropped (ref :751 via :772,786) */
 #define DASH_ERR_CTZ0 4u      /* ctz(0) on an EM entry: dropped (ref :209,451) */
 #define DASH_ERR_DEADLOCK 8u  /* quiescent with a node still waiting */
@@ -64,7 +66,9 @@ enum dash_txn {
 };
 
 /* flags */
-#define DASH_KEEP_STATE 1u /* write full final node state (needed by dash_read_state) */
+#define DASH_KEEP_STATE 1u    /* write full final node state (needed by dash_read_state) */
+#define DASH_TIER_FROM_32 2u  /* start at queue depth 32 (testing: exercises that kernel) */
+#define DASH_TIER_FROM_256 4u /* run every system at depth 256 directly */
 
 typedef struct dash_cfg {
     uint32_t num_procs;   /* NUM_PROCS (ref :6): 4 or 8 */
@@ -98,6 +102,7 @@ typedef struct dash_stats {
     uint64_t dropped;            /* messages dropped */
     uint64_t max_depth;          /* deepest queue after any delivery */
     double kernel_ms;            /* simulation kernel time (HIP events, engine stream) */
+    uint64_t tier_systems[3];    /* systems simulated at queue depth 16, 32, 256 */
 } dash_stats;
 
 /* Synthetic trace generator (counter-based, identical host spec in DESIGN.md §gen). */

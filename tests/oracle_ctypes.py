@@ -127,7 +127,7 @@ def load_test_dir(d, num_procs=4, max_instr=32):
 
 # ---------------------------------------------------------------- runs
 
-def run_system(trace, lens, num_procs=4, cache_size=4, ring_depth=32, max_rounds=0, log=False):
+def run_system(trace, lens, num_procs=4, cache_size=4, ring_depth=256, max_rounds=0, log=False):
     trace = np.ascontiguousarray(trace, dtype=np.uint16)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     cfg = OrcCfg(num_procs, cache_size, ring_depth, max_rounds)
@@ -154,7 +154,7 @@ def gen_system(seed, sys, num_procs=8, length=64, kind=0, locality=0):
 
 
 def run_batch(seed, first, count, num_procs=8, cache_size=4, length=64, kind=0, locality=0,
-              ring_depth=32, threads=1, max_rounds=0):
+              ring_depth=256, threads=1, max_rounds=0):
     cfg = OrcCfg(num_procs, cache_size, ring_depth, max_rounds)
     g = OrcGen(seed, kind, locality, length, num_procs)
     dig = np.zeros(count, dtype=np.uint64)

@@ -56,10 +56,10 @@ def state_arrays(nodes, N, CS):
     return out
 
 
-def check_batch(dash, packed, lens, N, CS, max_rounds=0):
+def check_batch(dash, packed, lens, N, CS, max_rounds=0, flags=0):
     nsys = packed.shape[0]
     with dash.Engine(nsys, num_procs=N, cache_size=CS, max_instr=packed.shape[2], keep_state=True,
-                     max_rounds=max_rounds) as eng:
+                     max_rounds=max_rounds, flags=flags) as eng:
         eng.load_traces(packed, lens)
         stats = eng.run()
         dig, rnd, err = eng.read_results()
@@ -67,7 +67,7 @@ def check_batch(dash, packed, lens, N, CS, max_rounds=0):
         rounds_total = 0
         instr_total = 0
         for s in range(nsys):
-            res = run_system(packed[s], lens[s], num_procs=N, cache_size=CS, ring_depth=32,
+            res = run_system(packed[s], lens[s], num_procs=N, cache_size=CS, ring_depth=256,
                              max_rounds=max_rounds or (1024 + 256 * packed.shape[2]))
             gpu_nodes = eng.read_state(s)
             assert state_arrays(gpu_nodes, N, CS) == state_arrays(res.node, N, CS), f"system {s}"
@@ -124,6 +124,25 @@ def test_contention_and_small_address_space(dash, N):
     rng = np.random.default_rng(77 + N)
     packed, lens = random_batch(rng, 128, N, 48, block_span=4, hot_frac=0.7)
     check_batch(dash, packed, lens, N, 4)
+
+
+# contention systems (generator seed 0x5EED, 4096 instr/node) whose queues exceed 16 (oracle)
+DEEP_SYSTEMS = [16, 67, 105, 199, 230, 236, 285, 309, 332]
+
+
+@pytest.mark.parametrize("flags", [0, 2, 4])
+def test_queue_depth_tiers(dash, flags):
+    """Deep queues: systems that would fill the 16-deep LDS rings are handed to
+    the 32-deep tier (and, from there, 256) and re-simulated from scratch; every
+    tier's kernel must give the oracle's result (queue capacity 256)."""
+    ids = DEEP_SYSTEMS + [0, 1, 2, 3, 4, 5, 6]
+    L = 4096
+    packed = np.stack([oracle_ctypes.gen_system(0x5EED, s, 8, L, kind=1) for s in ids])
+    lens = np.full((len(ids), 8), L, np.uint32)
+    stats = check_batch(dash, packed, lens, 8, 4, flags=flags)
+    if flags == 0:
+        assert stats["tier_systems"][:2] == [len(ids), len(DEEP_SYSTEMS)]
+    assert stats["max_depth"] > 16
 
 
 def test_long_traces_window_refill(dash):

@@ -20,10 +20,10 @@ struct dash_ctx {
     dash_cfg cfg{};
     uint32_t seg = 0;       // lanes per system (next pow2 of num_procs)
     uint64_t groups = 0;    // waves (64/seg systems each)
-    uint32_t nchunks = 0;   // 8-instruction chunks per lane
+    uint32_t nchunks = 0;   // 4-instruction chunks per lane
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    uint4* d_trace = nullptr;
+    uint2* d_trace = nullptr;
     uint32_t* d_lens = nullptr;
     uint64_t* d_digests = nullptr;
     uint32_t* d_rounds = nullptr;
@@ -31,6 +31,9 @@ struct dash_ctx {
     uint32_t* d_state = nullptr;
     uint32_t* d_hist = nullptr;
     unsigned long long* d_stats = nullptr;
+    uint32_t* d_list[2] = {nullptr, nullptr};  // overflow hand-off lists (ping-pong)
+    uint32_t* d_count = nullptr;
+    uint64_t tier_systems[3] = {0, 0, 0};      // systems run per queue-depth tier, last run
     bool loaded = false;
     bool ran = false;
     char msg[256] = {0};
@@ -76,6 +79,9 @@ static void release(dash_t* h) {
     (void)hipFree(h->d_state);
     (void)hipFree(h->d_hist);
     (void)hipFree(h->d_stats);
+    (void)hipFree(h->d_list[0]);
+    (void)hipFree(h->d_list[1]);
+    (void)hipFree(h->d_count);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -101,7 +107,7 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     h->seg = next_pow2(N);
     const uint64_t spw = 64 / h->seg;
     h->groups = (cfg->num_systems + spw - 1) / spw;
-    h->nchunks = (cfg->max_instr + 7) / 8;
+    h->nchunks = (cfg->max_instr + dash::CHUNK_INSTR - 1) / dash::CHUNK_INSTR;
     int rc = DASH_OK;
     auto chk = [&](hipError_t e, const char* what) {
         if (e != hipSuccess && rc == DASH_OK)
@@ -123,18 +129,20 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     chk(hipEventCreate(&h->ev1), "hipEventCreate");
     const uint64_t nsys = cfg->num_systems;
     const uint64_t trace_words = h->groups * (uint64_t)std::max<uint32_t>(h->nchunks, 1) * 64;
-    chk(hipMalloc(&h->d_trace, trace_words * sizeof(uint4)), "hipMalloc(trace)");
+    chk(hipMalloc(&h->d_trace, trace_words * sizeof(uint2)), "hipMalloc(trace)");
     chk(hipMalloc(&h->d_lens, std::max<uint64_t>(nsys * N, 1) * sizeof(uint32_t)), "hipMalloc(lens)");
     chk(hipMalloc(&h->d_digests, std::max<uint64_t>(nsys, 1) * sizeof(uint64_t)), "hipMalloc(digests)");
     chk(hipMalloc(&h->d_rounds, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(rounds)");
     chk(hipMalloc(&h->d_errors, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(errors)");
     chk(hipMalloc(&h->d_stats, dash::STAT_WORDS * sizeof(unsigned long long)), "hipMalloc(stats)");
-    if (cfg->flags & DASH_KEEP_STATE) {
+    chk(hipMalloc(&h->d_hist, std::max<uint64_t>(nsys * N, 1) * 13 * sizeof(uint32_t)), "hipMalloc(hist)");
+    chk(hipMalloc(&h->d_list[0], std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(list)");
+    chk(hipMalloc(&h->d_list[1], std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(list)");
+    chk(hipMalloc(&h->d_count, 2 * sizeof(uint32_t)), "hipMalloc(count)");
+    if (cfg->num_systems > 0xFFFFFFFFull) rc = fail(h, DASH_EINVAL, "more than 2^32 systems");
+    if (cfg->flags & DASH_KEEP_STATE)
         chk(hipMalloc(&h->d_state, std::max<uint64_t>(nsys * N, 1) * (16 + CS) * sizeof(uint32_t)),
             "hipMalloc(state)");
-        chk(hipMalloc(&h->d_hist, std::max<uint64_t>(nsys * N, 1) * 13 * sizeof(uint32_t)),
-            "hipMalloc(hist)");
-    }
     if (rc != DASH_OK) {
         fprintf(stderr, "dash_create: %s\n", h->msg);
         dash_destroy(h);
@@ -154,7 +162,8 @@ int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const u
             return fail(h, DASH_EINVAL, "trace %llu longer than max_instr", (unsigned long long)i);
     // lane-interleaved layout: [group][chunk][lane][8 x u16]
     const uint64_t words = h->groups * (uint64_t)h->nchunks * 64;
-    std::vector<uint16_t> host(words * 8, 0);
+    constexpr uint32_t C = dash::CHUNK_INSTR;
+    std::vector<uint16_t> host(words * C, 0);
     for (uint64_t s = 0; s < num_systems; s++) {
         const uint64_t g = s / (64 / P);
         const uint32_t lane0 = (uint32_t)(s % (64 / P)) * P;
@@ -165,13 +174,13 @@ int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const u
                 if (((w >> 12) & 7u) >= N)
                     return fail(h, DASH_EADDR, "system %llu node %u: address 0x%02X homed on node >= %u",
                                 (unsigned long long)s, t, (w >> 8) & 0x7F, N);
-                host[((g * h->nchunks + i / 8) * 64 + lane0 + t) * 8 + (i & 7)] = w;
+                host[((g * h->nchunks + i / C) * 64 + lane0 + t) * C + (i % C)] = w;
             }
         }
     }
     HIPCHK(h, hipSetDevice(h->cfg.device));
     if (words)
-        HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 16, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 8, hipMemcpyHostToDevice, h->stream));
     if (num_systems)
         HIPCHK(h, hipMemcpyAsync(h->d_lens, lens, num_systems * N * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -220,11 +229,39 @@ int dash_run(dash_t* h, dash_stats* stats) {
     a.errors = h->d_errors;
     a.state = h->d_state;
     a.hist_node = h->d_hist;
+    a.keep = (h->cfg.flags & DASH_KEEP_STATE) ? 1u : 0u;
     a.stats = h->d_stats;
+    const uint64_t spw = 64 / h->seg;
     HIPCHK(h, hipSetDevice(h->cfg.device));
     HIPCHK(h, hipMemsetAsync(h->d_stats, 0, dash::STAT_WORDS * sizeof(unsigned long long), h->stream));
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-    HIPCHK(h, dash::launch_sim(a, h->seg, h->cfg.cache_size, h->groups, h->stream));
+    // queue-depth tiers: every system runs at the first depth; systems that would
+    // overflow it are listed and re-run from scratch at the next depth (exact:
+    // the lockstep schedule is deterministic); the last tier drops like the reference
+    uint64_t todo = h->cfg.num_systems;
+    const uint32_t* list = nullptr;
+    const int first = (h->cfg.flags & DASH_TIER_FROM_256) ? 2 : (h->cfg.flags & DASH_TIER_FROM_32) ? 1 : 0;
+    for (int tier = 0; tier < 3; ++tier) h->tier_systems[tier] = 0;
+    for (int tier = first; tier < 3; ++tier) {
+        h->tier_systems[tier] = todo;
+        if (todo == 0) continue;
+        uint32_t* out = h->d_list[tier & 1];
+        uint32_t* cnt = h->d_count + (tier & 1);
+        a.sys_list = list;
+        a.list_len = todo;
+        a.final_tier = tier == 2 ? 1u : 0u;
+        a.ovf_list = out;
+        a.ovf_count = cnt;
+        HIPCHK(h, hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
+        HIPCHK(h, dash::launch_sim(a, h->seg, h->cfg.cache_size, dash::RING_TIERS[tier], (todo + spw - 1) / spw,
+                                   h->stream));
+        if (tier == 2) break;
+        uint32_t next = 0;
+        HIPCHK(h, hipMemcpyAsync(&next, cnt, sizeof next, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        todo = next;
+        list = out;
+    }
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     unsigned long long s[dash::STAT_WORDS];
     HIPCHK(h, hipMemcpyAsync(s, h->d_stats, sizeof s, hipMemcpyDeviceToHost, h->stream));
@@ -244,6 +281,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
         stats->dropped = s[dash::STAT_DROPS];
         stats->max_depth = s[dash::STAT_MAXDEPTH];
         stats->kernel_ms = ms;
+        for (int k = 0; k < 3; k++) stats->tier_systems[k] = h->tier_systems[k];
     }
     return DASH_OK;
 }
@@ -298,7 +336,7 @@ int dash_read_state(dash_t* h, uint64_t sys, dash_node_state* out) {
 int dash_read_hist(dash_t* h, uint64_t sys, uint32_t* hist) {
     if (!h || !hist) return DASH_EINVAL;
     if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
-    if (!h->d_hist) return fail(h, DASH_ESTATE, "created without DASH_KEEP_STATE");
+    if (!(h->cfg.flags & DASH_KEEP_STATE)) return fail(h, DASH_ESTATE, "created without DASH_KEEP_STATE");
     if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
     const uint32_t N = h->cfg.num_procs;
     std::vector<uint32_t> w((size_t)N * 13);

@@ -27,23 +27,29 @@ enum : uint32_t {
 };
 
 struct SimArgs {
-    const uint4* trace;       // [group][chunk][64] x 16 B (8 packed instructions)
+    const uint2* trace;       // [group][chunk][64] x 8 B (4 packed instructions)
     const uint32_t* lens;     // [sys * N + node]
     uint64_t nsys;
     uint32_t nchunks;
     uint32_t num_procs;
     uint32_t max_rounds;
-    uint32_t _pad;
+    uint32_t final_tier;      // 1: queue overflow drops (reference semantics); 0: hand off
+    const uint32_t* sys_list; // systems to (re)run; nullptr = all systems in order
+    uint64_t list_len;
+    uint32_t* ovf_list;       // systems handed to the next queue-depth tier
+    uint32_t* ovf_count;
     uint64_t* digests;        // [sys]
     uint32_t* rounds;         // [sys]
     uint32_t* errors;         // [sys]
-    uint32_t* state;          // optional [(sys*N+node)*(16+CS)] raw LDS words
-    uint32_t* hist_node;      // optional [(sys*N+node)*13]
+    uint32_t* state;          // optional [(sys*N+node)*(16+CS)] directory/cache words
+    uint32_t* hist_node;      // [(sys*N+node)*13]; written when keep or on counter drain
+    uint32_t keep;
+    uint32_t _pad;
     unsigned long long* stats;  // [STAT_WORDS]
 };
 
 struct GenArgs {
-    uint4* trace;
+    uint2* trace;
     uint32_t* lens;
     uint64_t nsys;
     uint64_t ngroups;
@@ -57,7 +63,12 @@ struct GenArgs {
     uint32_t len;
 };
 
-hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint64_t groups, hipStream_t s);
+hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring, uint64_t groups,
+                      hipStream_t s);
+
+// queue-depth tiers: first pass, re-run of overflowed systems, final (reference MSG_BUFFER_SIZE)
+constexpr uint32_t RING_TIERS[3] = {16, 32, 256};
+constexpr uint32_t CHUNK_INSTR = 4;  // instructions per 8-B trace chunk
 hipError_t launch_gen(const GenArgs& g, hipStream_t s);
 
 }  // namespace dash

@@ -7,15 +7,20 @@
 // Mapping:
 //   * one lane = one node, P = next_pow2(N) lanes = one system, a wave64 holds
 //     64/P systems; one wave per workgroup, so all per-system state sits in the
-//     workgroup's LDS and every per-lane access is bank-conflict free
-//     (arrays are [slot][lane], bank = lane % 32);
+//     workgroup's LDS ([slot][lane] arrays: every per-lane access is bank-conflict
+//     free) or in lane registers;
 //   * lockstep rounds: each lane pops one message or issues one instruction,
 //     then all sends of the round are delivered with a segmented prefix sum
 //     over the P lanes (lowest sender first, program order inside a sender)
 //     straight into the receivers' LDS rings -- no locks, no atomics;
-//   * traces stream from HBM in a lane-interleaved layout
-//     [group][chunk][lane][8 x u16] into a 3-chunk LDS window, refilled every
-//     8 rounds so no global-load latency sits on the round's critical path.
+//   * queue depth is tiered: a pass with RING-deep queues halts and lists any
+//     system that would overflow; the listed systems are re-simulated from
+//     scratch with deeper queues, the last tier being the reference's 256
+//     (MSG_BUFFER_SIZE, ref :9). The schedule is deterministic, so a system that
+//     never fills its queues is identical at every depth;
+//   * traces stream from HBM in a lane-interleaved layout [group][chunk][lane]
+//     (4 instructions = 8 B per lane-chunk) into a 3-chunk LDS window, refilled
+//     every 4 rounds, so no global-load latency sits on a round's critical path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -43,9 +48,9 @@ constexpr uint64_t TA_BASE = ((uint64_t)T_RID << (4 * T_UPG)) | ((uint64_t)T_FIA
                              ((uint64_t)T_FLUSH << (4 * T_WBINT)) | ((uint64_t)T_ES << (4 * T_ES)) |
                              ((uint64_t)T_RR << (4 * T_ISSUE_R)) | ((uint64_t)T_WRQ << (4 * T_ISSUE_W));
 
-constexpr uint32_t RING = 32;    // per-node queue depth (ref MSG_BUFFER_SIZE 256)
-constexpr uint32_t WIN = 3;      // trace window chunks per lane
-constexpr uint32_t PERIOD = 8;   // window refill period in rounds (= chunk length)
+constexpr uint32_t WIN = 3;        // trace window chunks per lane
+constexpr uint32_t CHUNK = 4;      // instructions per chunk (8 B)
+constexpr uint32_t HIST_FLUSH = 0x7FFF;  // u16 histogram counters drain every 32768 rounds
 
 // message word (ref `message`, :70-79, 20 B -> 4 B):
 //   [3:0] type  [6:4] sender  [15:8] address  [23:16] value | bitVector
@@ -64,76 +69,90 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
     return k;
 }
 
-// spread 8 bits into the low bit of 8 nibbles
-__device__ __forceinline__ uint32_t spread_nibbles(uint32_t x) {
-    x = (x | (x << 12)) & 0x000F000Fu;
-    x = (x | (x << 6)) & 0x03030303u;
-    x = (x | (x << 3)) & 0x11111111u;
-    return x;
-}
-
-template <int CS>
-struct Lds {
-    static constexpr uint32_t ENT = 0;                   // [16][64]  mem | bv<<8 | ds<<16
-    static constexpr uint32_t CAC = ENT + 16 * 64;       // [CS][64]  addr | val<<8 | st<<16
-    static constexpr uint32_t RNG = CAC + CS * 64;       // [32][64]  message words
-    static constexpr uint32_t WND = RNG + RING * 64;     // [3][64][4] trace chunks (16 B)
-    static constexpr uint32_t HST = WND + WIN * 64 * 4;  // [13][64]  handled per type
-    static constexpr uint32_t WORDS = HST + 13 * 64;
-    static_assert(WND % 4 == 0, "window must be 16-B aligned");
-};
-
-// byte k of a u64 held as two u32 halves
-__device__ __forceinline__ uint32_t byte_of(uint32_t lo, uint32_t hi, uint32_t k) {
-    return ((k < 4 ? lo : hi) >> (8 * (k & 3))) & 0xFFu;
-}
-
-// 4 bits -> low bit of 4 bytes
-__device__ __forceinline__ uint32_t spread4(uint32_t x) { return ((x & 15u) * 0x00204081u) & 0x01010101u; }
-
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
 }
 
-// segmented (P lanes) exclusive prefix sum and total of byte-packed counters,
-// on the VALU (DPP row shifts / quad perms / half-row mirror): no LDS traffic
-template <int P>
-__device__ __forceinline__ void seg_scan_total(uint32_t lo, uint32_t hi, uint32_t t, uint32_t& ex_lo,
-                                               uint32_t& ex_hi, uint32_t& to_lo, uint32_t& to_hi) {
-    uint32_t il = lo, ih = hi;
-    if constexpr (P >= 2) {
-        const uint32_t yl = dpp<0x111>(il), yh = dpp<0x111>(ih);  // row_shr:1
-        if (t >= 1) { il += yl; ih += yh; }
+// ---- per-receiver counters packed FW bits per field (one field per node of the system) ----
+template <int P, int FW>
+struct Fields {
+    static constexpr int PER = 32 / FW;                  // fields per register
+    static constexpr int NR = (P + PER - 1) / PER;       // registers
+    static constexpr uint32_t LSB = FW == 8 ? 0x01010101u : 0x00010001u;
+    static constexpr uint32_t FMASK = (1u << FW) - 1u;
+    uint32_t r[NR];
+
+    __device__ __forceinline__ uint32_t get(uint32_t d) const {
+        uint32_t v = r[0];
+#pragma unroll
+        for (int k = 1; k < NR; ++k) v = (d / PER == (uint32_t)k) ? r[k] : v;
+        return (v >> (FW * (d % PER))) & FMASK;
     }
-    if constexpr (P >= 4) {
-        const uint32_t yl = dpp<0x112>(il), yh = dpp<0x112>(ih);  // row_shr:2
-        if (t >= 2) { il += yl; ih += yh; }
+    // bits of `m` (bit i = node i) -> one in field i
+    __device__ __forceinline__ static Fields spread(uint32_t m) {
+        Fields f;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            const uint32_t x = m >> (k * PER);
+            f.r[k] = FW == 8 ? (((x & 15u) * 0x00204081u) & 0x01010101u)
+                             : (((x & 3u) * 0x00008001u) & 0x00010001u);
+        }
+        return f;
     }
-    if constexpr (P >= 8) {
-        const uint32_t yl = dpp<0x114>(il), yh = dpp<0x114>(ih);  // row_shr:4
-        if (t >= 4) { il += yl; ih += yh; }
+    __device__ __forceinline__ void add_one(bool v, uint32_t d) {
+        const uint32_t one = v ? (1u << (FW * (d % PER))) : 0u;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) r[k] += (d / PER == (uint32_t)k) ? one : 0u;
     }
-    ex_lo = il - lo;
-    ex_hi = ih - hi;
-    uint32_t sl = lo, sh = hi;
-    if constexpr (P >= 2) { sl += dpp<0xB1>(sl); sh += dpp<0xB1>(sh); }    // quad_perm [1,0,3,2]
-    if constexpr (P >= 4) { sl += dpp<0x4E>(sl); sh += dpp<0x4E>(sh); }    // quad_perm [2,3,0,1]
-    if constexpr (P >= 8) { sl += dpp<0x141>(sl); sh += dpp<0x141>(sh); }  // row_half_mirror
-    to_lo = sl;
-    to_hi = sh;
+};
+
+// segmented (P lanes) exclusive prefix sum and total, on the VALU (DPP row
+// shifts, quad perms, half-row mirror): no LDS or permute traffic
+template <int P, int FW>
+__device__ __forceinline__ void seg_scan_total(const Fields<P, FW>& c, uint32_t t, Fields<P, FW>& ex,
+                                               Fields<P, FW>& tot) {
+#pragma unroll
+    for (int k = 0; k < Fields<P, FW>::NR; ++k) {
+        uint32_t il = c.r[k];
+        if constexpr (P >= 2) { const uint32_t y = dpp<0x111>(il); il += t >= 1 ? y : 0u; }  // row_shr:1
+        if constexpr (P >= 4) { const uint32_t y = dpp<0x112>(il); il += t >= 2 ? y : 0u; }  // row_shr:2
+        if constexpr (P >= 8) { const uint32_t y = dpp<0x114>(il); il += t >= 4 ? y : 0u; }  // row_shr:4
+        ex.r[k] = il - c.r[k];
+        uint32_t s = c.r[k];
+        if constexpr (P >= 2) s += dpp<0xB1>(s);   // quad_perm [1,0,3,2]
+        if constexpr (P >= 4) s += dpp<0x4E>(s);   // quad_perm [2,3,0,1]
+        if constexpr (P >= 8) s += dpp<0x141>(s);  // row_half_mirror
+        tot.r[k] = s;
+    }
 }
 
-// per byte: min(x, 32), x <= 127
-__device__ __forceinline__ uint32_t clamp32_bytes(uint32_t x) {
-    const uint32_t over = ((x + 0x5F5F5F5Fu) & 0x80808080u) >> 7;  // byte >= 33
-    const uint32_t m = over * 0xFFu;
-    return (x & ~m) | (0x20202020u & m);
+// per field: min(x, RING); fields hold at most RING + 2P
+template <int FW, uint32_t RING>
+__device__ __forceinline__ uint32_t clamp_fields(uint32_t x) {
+    constexpr uint32_t TOP = 1u << (FW - 1);
+    constexpr uint32_t LSB = FW == 8 ? 0x01010101u : 0x00010001u;
+    constexpr uint32_t bias = (TOP - 1u - RING) * LSB;
+    const uint32_t over = ((x + bias) & (TOP * LSB)) >> (FW - 1);  // field > RING
+    const uint32_t m = (over << FW) - over;                        // field mask where over
+    return (x & ~m) | ((RING * LSB) & m);
 }
 
-template <int P, int CS>
+template <int CS, uint32_t RING>
+struct Lds {  // 32-bit word offsets
+    static constexpr uint32_t ENT = 0;                      // u16 [16][64]  mem | bitVector<<8
+    static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8
+    static constexpr uint32_t RNG = CAC + CS * 64 / 2;      // u32 [RING][64] message words
+    static constexpr uint32_t WND = RNG + RING * 64;        // u16x4 [WIN][64] trace chunks
+    static constexpr uint32_t HST = WND + WIN * 64 * 2;     // u32 [7][64]   two u16 counters
+    static constexpr uint32_t WORDS = HST + 7 * 64;
+};
+
+template <int P, int CS, uint32_t RING>
 __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
-    using L = Lds<CS>;
+    using L = Lds<CS, RING>;
+    constexpr int FW = RING <= 64 ? 8 : 16;
+    using F = Fields<P, FW>;
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
     __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS];
@@ -142,49 +161,66 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     const uint32_t lane = threadIdx.x;
     const uint32_t t = lane & (P - 1);  // node id (threadId in the reference)
     const uint32_t seg = lane - t;
-    const uint64_t sys = (uint64_t)blockIdx.x * SPW + lane / P;
+    const uint64_t slot_id = (uint64_t)blockIdx.x * SPW + lane / P;
     const uint32_t N = a.num_procs;
-    const bool live = sys < a.nsys && t < N;
+    bool live;
+    uint64_t sys;
+    if (a.sys_list) {  // re-run of systems that overflowed a shallower tier
+        live = slot_id < a.list_len && t < N;
+        sys = slot_id < a.list_len ? a.sys_list[slot_id] : 0;
+    } else {
+        live = slot_id < a.nsys && t < N;
+        sys = slot_id;
+    }
     uint32_t len = live ? a.lens[sys * N + t] : 0u;
     const uint32_t rcv_mask = (1u << N) - 1u;
+    uint32_t* const hist_row = a.hist_node + (sys * N + t) * 13;
 
-    // initializeProcessor's state part (ref :808-820)
+    // initializeProcessor's state part (ref :808-820); directory/line states
+    // live in two lane registers (2 bits per entry), the rest in LDS
 #pragma unroll
-    for (uint32_t b = 0; b < 16; ++b)
-        lds[L::ENT + b * 64 + lane] = ((20u * t + b) & 0xFFu) | (D_U << 16);
+    for (uint32_t b = 0; b < 16; ++b) lds16[L::ENT * 2 + b * 64 + lane] = (uint16_t)((20u * t + b) & 0xFFu);
 #pragma unroll
-    for (uint32_t i = 0; i < CS; ++i) lds[L::CAC + i * 64 + lane] = 0xFFu | (ST_I << 16);
+    for (uint32_t i = 0; i < CS; ++i) lds16[L::CAC * 2 + i * 64 + lane] = 0xFFu;
 #pragma unroll
-    for (uint32_t k = 0; k < 13; ++k) lds[L::HST + k * 64 + lane] = 0u;
+    for (uint32_t k = 0; k < 7; ++k) lds[L::HST + k * 64 + lane] = 0u;
+    uint32_t dsv = 0xAAAAAAAAu;  // 16 x U
+    uint32_t cst = 0xFFFFFFFFu;  // CS x INVALID
 
     // trace window prefill: chunks 0..WIN-1 landed, chunk WIN pending in registers
-    const uint4* tr = a.trace + (uint64_t)blockIdx.x * a.nchunks * 64 + lane;
-    const uint32_t nch = (len + 7u) >> 3;
+    const uint2* tr = a.trace + ((sys / SPW) * a.nchunks) * 64 + (sys % SPW) * P + t;
+    const uint32_t nch = (len + CHUNK - 1) / CHUNK;
 #pragma unroll
     for (uint32_t c = 0; c < WIN; ++c)
-        if (c < nch) *reinterpret_cast<uint4*>(&lds[L::WND + (c * 64 + lane) * 4]) = tr[c * 64];
+        if (c < nch) *reinterpret_cast<uint2*>(&lds[L::WND + (c * 64 + lane) * 2]) = tr[c * 64];
     uint32_t pend_idx = WIN;
-    uint4 pend = make_uint4(0, 0, 0, 0);
+    uint2 pend = make_uint2(0, 0);
     if (pend_idx < nch) pend = tr[pend_idx * 64];
 
-    // Every lane of a system carries the queue state of ALL the system's nodes,
-    // byte r = node r's count / tail (updated identically in every lane), so a
-    // sender finds its receiver's free slot without a cross-lane read.
-    uint32_t cnt_lo = 0, cnt_hi = 0, tail_lo = 0, tail_hi = 0;
+    // Every lane of a system carries the queue count and tail of ALL the
+    // system's nodes (one field per node, updated identically in every lane),
+    // so a sender finds its receiver's free slot without a cross-lane read.
+    F cnt, tail;
+#pragma unroll
+    for (int k = 0; k < F::NR; ++k) cnt.r[k] = tail.r[k] = 0u;
     uint32_t pc = 0, waiting = 0, last_val = 0;
     uint32_t err = 0, rounds = 0, maxd = 0, drops = 0;
+    bool flushed = false;
     const uint32_t cap = a.max_rounds;
+    const bool final_tier = a.final_tier != 0;
 
     for (uint32_t r = 0;; ++r) {
-        // ---- quiescence / round cap on start-of-round state ----
-        uint32_t my_cnt = byte_of(cnt_lo, cnt_hi, t);
+        // ---- quiescence / round cap / tier overflow, on start-of-round state ----
+        uint32_t my_cnt = cnt.get(t);
         bool can_issue = !waiting && pc < len;
         const uint64_t act = __ballot(my_cnt != 0 || can_issue);
         if (act == 0) break;
         bool sys_act = ((uint32_t)(act >> seg) & SEGMASK) != 0;
-        if (sys_act && rounds >= cap) {  // every lane of a system agrees (same `rounds`)
-            err |= DASH_ERR_ROUNDCAP_D;
-            cnt_lo = cnt_hi = 0;
+        const bool sys_ovf = !final_tier && (((uint32_t)(__ballot((err & DASH_ERR_OVERFLOW_D) != 0) >> seg) & SEGMASK) != 0);
+        if (sys_act && (rounds >= cap || sys_ovf)) {  // all lanes of a system agree
+            err |= rounds >= cap ? DASH_ERR_ROUNDCAP_D : 0u;
+#pragma unroll
+            for (int k = 0; k < F::NR; ++k) cnt.r[k] = 0u;
             my_cnt = 0;
             len = pc;
             waiting = 0;
@@ -193,35 +229,49 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         }
         rounds += sys_act ? 1u : 0u;
 
-        // ---- trace window refill, wave-uniform every PERIOD rounds ----
-        if ((r & (PERIOD - 1)) == 0) {
-            if (pend_idx < nch && pend_idx < (pc >> 3) + WIN) {
-                *reinterpret_cast<uint4*>(&lds[L::WND + ((pend_idx % WIN) * 64 + lane) * 4]) = pend;
+        // ---- wave-uniform housekeeping: trace window refill, histogram drain ----
+        if ((r & (CHUNK - 1)) == 0) {
+            if (pend_idx < nch && pend_idx < pc / CHUNK + WIN) {
+                *reinterpret_cast<uint2*>(&lds[L::WND + ((pend_idx % WIN) * 64 + lane) * 2]) = pend;
                 ++pend_idx;
                 if (pend_idx < nch) pend = tr[pend_idx * 64];
+            }
+            if ((r & HIST_FLUSH) == HIST_FLUSH - (CHUNK - 1)) {
+#pragma unroll
+                for (uint32_t k = 0; k < 7; ++k) {
+                    const uint32_t w = lds[L::HST + k * 64 + lane];
+                    lds[L::HST + k * 64 + lane] = 0u;
+                    if (live) {
+                        hist_row[2 * k] = (flushed ? hist_row[2 * k] : 0u) + (w & 0xFFFFu);
+                        if (k < 6) hist_row[2 * k + 1] = (flushed ? hist_row[2 * k + 1] : 0u) + (w >> 16);
+                    }
+                }
+                flushed = true;
             }
         }
 
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
         const bool has_msg = my_cnt != 0;
-        const uint32_t head = (byte_of(tail_lo, tail_hi, t) - my_cnt) & (RING - 1);
+        const uint32_t head = (tail.get(t) - my_cnt) & (RING - 1);
         const uint32_t m = lds[L::RNG + head * 64 + lane];
-        const uint32_t ins = lds16[(L::WND * 2) + (((pc >> 3) % WIN) * 64 + lane) * 8 + (pc & 7u)];
+        const uint32_t ins = lds16[L::WND * 2 + (((pc / CHUNK) % WIN) * 64 + lane) * CHUNK + (pc & (CHUNK - 1))];
         const bool do_issue = !has_msg && can_issue;
         pc += do_issue ? 1u : 0u;
-        const uint32_t pops = (uint32_t)(__ballot(has_msg) >> seg) & SEGMASK;
-        const uint32_t cp_lo = cnt_lo - spread4(pops), cp_hi = cnt_hi - spread4(pops >> 4);
+        const F pops = F::spread((uint32_t)(__ballot(has_msg) >> seg) & SEGMASK);
+        F cp;  // queue counts after this round's pops
+#pragma unroll
+        for (int k = 0; k < F::NR; ++k) cp.r[k] = cnt.r[k] - pops.r[k];
 
         const uint32_t type = has_msg ? (m & 15u) : (do_issue ? (T_ISSUE_R + (ins >> 15)) : T_IDLE);
         const uint32_t addr = has_msg ? ((m >> 8) & 0xFFu) : ((ins >> 8) & 0x7Fu);
         const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         const uint32_t idx = b & (CS - 1);
-        const uint32_t ent = lds[L::ENT + b * 64 + lane];
-        const uint32_t line = lds[L::CAC + idx * 64 + lane];
+        const uint32_t e16 = lds16[L::ENT * 2 + b * 64 + lane];
+        const uint32_t c16 = lds16[L::CAC * 2 + idx * 64 + lane];
 
-        const uint32_t mem = ent & 0xFFu, bv = (ent >> 8) & 0xFFu, ds = (ent >> 16) & 3u;
-        const uint32_t laddr = line & 0xFFu, lval = (line >> 8) & 0xFFu, lst = (line >> 16) & 3u;
+        const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
+        const uint32_t laddr = c16 & 0xFFu, lval = c16 >> 8, lst = (cst >> (2 * idx)) & 3u;
         const uint32_t msender = (m >> 4) & 7u, mval = (m >> 16) & 0xFFu;
         const uint32_t msr = (m >> 24) & 7u, mds_s = (m >> 27) & 1u;
         const uint32_t ival = ins & 0xFFu;
@@ -265,7 +315,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         uint32_t nst = ((any(B(T_INV)) & same) | any(B(T_WBINV))) ? ST_I : lst;  // :396-398 :501
         nst = any(B(T_WBINT)) ? ST_S : nst;                                    // :284
         nst = (any(B(T_ES)) & (!tH | (es_one & (es_own == H)))) ? ST_E : nst;  // :558 :586
-        const uint32_t nline = fill ? (addr | (fval << 8) | (fst << 16)) : ((line & ~(3u << 16)) | (nst << 16));
+        nst = fill ? fst : nst;
         // handleCacheReplacement of the refilled line (:767-804); REPLY_WR unconditional (:467)
         const bool ev = fill & (lst != ST_I) & (any(B(T_RWR)) | !same);
 
@@ -306,31 +356,28 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         err |= (oob ? DASH_ERR_OOB_D : 0u) | (ctz0 ? DASH_ERR_CTZ0_D : 0u);
         drops += (oob ? 1u : 0u) + (ctz0 ? 1u : 0u);
 
-        lds[L::ENT + b * 64 + lane] = nmem | (nbv << 8) | (nds << 16);
-        lds[L::CAC + idx * 64 + lane] = nline;
+        lds16[L::ENT * 2 + b * 64 + lane] = (uint16_t)(nmem | (nbv << 8));
+        lds16[L::CAC * 2 + idx * 64 + lane] = (uint16_t)(fill ? (addr | (fval << 8)) : c16);
+        dsv = (dsv & ~(3u << (2 * b))) | (nds << (2 * b));
+        cst = (cst & ~(3u << (2 * idx))) | (nst << (2 * idx));
         if (has_msg)
-            __hip_atomic_fetch_add(&lds[L::HST + (m & 15u) * 64 + lane], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&lds[L::HST + ((m & 15u) >> 1) * 64 + lane], 1u << (16 * (m & 1u)),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 
         // ---- end-of-round delivery: lowest sender first, program order within a sender ----
-        // per-receiver byte counts of this lane's sends, segmented exclusive scan + total
-        uint32_t c_lo = spread4(inv), c_hi = spread4(inv >> 4);
-        const uint32_t oneP = vP ? (1u << (8 * (dP & 3u))) : 0u;
-        const uint32_t oneB = vB ? (1u << (8 * (dB & 3u))) : 0u;
-        c_lo += (dP < 4u ? oneP : 0u) + (dB < 4u ? oneB : 0u);
-        c_hi += (dP < 4u ? 0u : oneP) + (dB < 4u ? 0u : oneB);
-        uint32_t ex_lo, ex_hi, to_lo, to_hi;
-        seg_scan_total<P>(c_lo, c_hi, t, ex_lo, ex_hi, to_lo, to_hi);
-        // free-slot cursor and fill level per receiver (bytes): tail + excl, count-after-pop + excl
-        const uint32_t sl_lo = tail_lo + ex_lo, sl_hi = tail_hi + ex_hi;
-        const uint32_t fl_lo = cp_lo + ex_lo, fl_hi = cp_hi + ex_hi;
-
+        F c = F::spread(inv), ex, tot;
+        c.add_one(vP, dP);
+        c.add_one(vB, dB);
+        seg_scan_total<P, FW>(c, t, ex, tot);
+        F sl, fl;  // per receiver: next free slot (tail + excl), fill level after earlier senders
+#pragma unroll
+        for (int k = 0; k < F::NR; ++k) {
+            sl.r[k] = tail.r[k] + ex.r[k];
+            fl.r[k] = cp.r[k] + ex.r[k];
+        }
         auto deliver = [&](bool v, uint32_t d, uint32_t w, uint32_t local) {
-            const uint32_t sh = 8u * (d & 3u);
-            const bool hi = d >= 4u;
-            const uint32_t fill_d = ((hi ? fl_hi : fl_lo) >> sh) & 0xFFu;
-            const uint32_t slot = ((((hi ? sl_hi : sl_lo) >> sh) & 0xFFu) + local) & (RING - 1);
-            const bool ok = fill_d + local < RING;
+            const uint32_t slot = (sl.get(d) + local) & (RING - 1);
+            const bool ok = fl.get(d) + local < RING;
             if (v & ok) lds[L::RNG + slot * 64 + seg + d] = w;
             const bool dropped = v & !ok;
             err |= dropped ? DASH_ERR_OVERFLOW_D : 0u;
@@ -349,44 +396,61 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         deliver(vB, dB, wA, (vA & (dP == dB)) ? 1u : 0u);
 
         // every lane: new counts = min(count - pop + arrivals, RING); tails advance by delivered
-        const uint32_t n_lo = clamp32_bytes(cp_lo + to_lo), n_hi = clamp32_bytes(cp_hi + to_hi);
-        tail_lo = (tail_lo + (n_lo - cp_lo)) & 0x1F1F1F1Fu;
-        tail_hi = (tail_hi + (n_hi - cp_hi)) & 0x1F1F1F1Fu;
-        cnt_lo = n_lo;
-        cnt_hi = n_hi;
-        maxd = max(maxd, byte_of(cnt_lo, cnt_hi, t));
+#pragma unroll
+        for (int k = 0; k < F::NR; ++k) {
+            const uint32_t n = clamp_fields<FW, RING>(cp.r[k] + tot.r[k]);
+            tail.r[k] = (tail.r[k] + (n - cp.r[k])) & ((RING - 1) * F::LSB);
+            cnt.r[k] = n;
+        }
+        maxd = max(maxd, cnt.get(t));
     }
 
     // ---- results ----
     if (waiting) err |= DASH_ERR_DEADLOCK_D;
-    uint64_t h = 0x243F6A8885A308D3ull ^ ((uint64_t)t << 56);
-    for (uint32_t b = 0; b < 16; ++b) h = fmix64(h ^ (uint64_t)lds[L::ENT + b * 64 + lane]);
-    for (uint32_t i = 0; i < CS; ++i) h = fmix64(h ^ ((uint64_t)lds[L::CAC + i * 64 + lane] | (1ull << 24)));
-    uint64_t dg = 0x9E3779B97F4A7C15ull;
     uint32_t serr = err;
+#pragma unroll
+    for (uint32_t n = 1; n < P; n <<= 1) serr |= __shfl_xor(serr, n, P);
+    // a non-final tier hands overflowed systems to the next tier: no outputs, no statistics
+    const bool handoff = !final_tier && (serr & DASH_ERR_OVERFLOW_D) != 0;
+    const bool report = live && !handoff;
+
+    uint32_t hcnt[13];
+#pragma unroll
+    for (uint32_t k = 0; k < 7; ++k) {
+        const uint32_t w = lds[L::HST + k * 64 + lane];
+        hcnt[2 * k] = (w & 0xFFFFu) + ((flushed && live) ? hist_row[2 * k] : 0u);
+        if (k < 6) hcnt[2 * k + 1] = (w >> 16) + ((flushed && live) ? hist_row[2 * k + 1] : 0u);
+    }
+    uint64_t h = 0x243F6A8885A308D3ull ^ ((uint64_t)t << 56);
+    for (uint32_t b = 0; b < 16; ++b)
+        h = fmix64(h ^ (uint64_t)(lds16[L::ENT * 2 + b * 64 + lane] | (((dsv >> (2 * b)) & 3u) << 16)));
+    for (uint32_t i = 0; i < CS; ++i)
+        h = fmix64(h ^ ((uint64_t)(lds16[L::CAC * 2 + i * 64 + lane] | (((cst >> (2 * i)) & 3u) << 16)) |
+                        (1ull << 24)));
+    uint64_t dg = 0x9E3779B97F4A7C15ull;
 #pragma unroll
     for (uint32_t n = 0; n < P; ++n) {
         const uint64_t hn = __shfl(h, seg + n);
         if (n < N) dg = fmix64(dg ^ hn);
-        serr |= __shfl(err, seg + n);
     }
-    if (live && t == 0) {
+    if (report && t == 0) {
         a.digests[sys] = dg;
         a.rounds[sys] = rounds;
         a.errors[sys] = serr;
     }
-    if (a.state && live) {
+    if (live && t == 0 && handoff) a.ovf_list[atomicAdd(a.ovf_count, 1u)] = (uint32_t)sys;
+    if (a.state && report) {
         uint32_t* st = a.state + (sys * N + t) * (16 + CS);
-        for (uint32_t b = 0; b < 16; ++b) st[b] = lds[L::ENT + b * 64 + lane];
-        for (uint32_t i = 0; i < CS; ++i) st[16 + i] = lds[L::CAC + i * 64 + lane];
+        for (uint32_t b = 0; b < 16; ++b)
+            st[b] = lds16[L::ENT * 2 + b * 64 + lane] | (((dsv >> (2 * b)) & 3u) << 16);
+        for (uint32_t i = 0; i < CS; ++i)
+            st[16 + i] = lds16[L::CAC * 2 + i * 64 + lane] | (((cst >> (2 * i)) & 3u) << 16);
     }
-    if (a.hist_node && live) {
-        uint32_t* hs = a.hist_node + (sys * N + t) * 13;
-        for (uint32_t k = 0; k < 13; ++k) hs[k] = lds[L::HST + k * 64 + lane];
-    }
+    if (report && (a.keep || flushed))
+        for (uint32_t k = 0; k < 13; ++k) hist_row[k] = hcnt[k];
 
     // ---- global statistics: wave reductions, one atomic per counter per wave ----
-    const bool head_lane = live && t == 0;
+    const bool head_lane = report && t == 0;
     unsigned long long* S = a.stats;
     auto wsum = [](uint64_t v) {
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -400,23 +464,23 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         return v;
     };
     for (uint32_t k = 0; k < 13; ++k) {
-        const uint64_t v = wsum(live ? lds[L::HST + k * 64 + lane] : 0u);
+        const uint64_t v = wsum(report ? hcnt[k] : 0u);
         if (lane == 0 && v) atomicAdd(&S[STAT_HIST + k], (unsigned long long)v);
     }
-    const uint64_t s_instr = wsum(live ? pc : 0u);
+    const uint64_t s_instr = wsum(report ? pc : 0u);
     const uint64_t s_rounds = wsum(head_lane ? rounds : 0u);
     const uint64_t m_rounds = wmax(head_lane ? rounds : 0u);
     const uint64_t s_sys = wsum(head_lane ? 1u : 0u);
     const uint64_t s_errsys = wsum((head_lane && serr) ? 1u : 0u);
-    const uint64_t s_drops = wsum(live ? drops : 0u);
-    const uint64_t m_depth = wmax(live ? maxd : 0u);
-    uint64_t ebits = live ? err : 0u;
+    const uint64_t s_drops = wsum(report ? drops : 0u);
+    const uint64_t m_depth = wmax(report ? maxd : 0u);
+    uint64_t ebits = report ? err : 0u;
     for (int o = 32; o > 0; o >>= 1) ebits |= __shfl_xor(ebits, o);
     if (lane == 0) {
-        atomicAdd(&S[STAT_INSTR], (unsigned long long)s_instr);
-        atomicAdd(&S[STAT_ROUNDS], (unsigned long long)s_rounds);
+        if (s_instr) atomicAdd(&S[STAT_INSTR], (unsigned long long)s_instr);
+        if (s_rounds) atomicAdd(&S[STAT_ROUNDS], (unsigned long long)s_rounds);
         atomicMax(&S[STAT_ROUNDS_MAX], (unsigned long long)m_rounds);
-        atomicAdd(&S[STAT_SYSTEMS], (unsigned long long)s_sys);
+        if (s_sys) atomicAdd(&S[STAT_SYSTEMS], (unsigned long long)s_sys);
         if (s_errsys) atomicAdd(&S[STAT_ERRSYS], (unsigned long long)s_errsys);
         if (ebits) atomicOr(&S[STAT_ERRBITS], (unsigned long long)ebits);
         if (s_drops) atomicAdd(&S[STAT_DROPS], (unsigned long long)s_drops);
@@ -424,7 +488,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     }
 }
 
-// ---- synthetic trace generator (spec: DESIGN.md §gen; host twin in oracle/) ----
+// ---- synthetic trace generator (spec: DESIGN.md §5; host twin in oracle/) ----
 __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
     const uint64_t total = g.ngroups * g.nchunks * 64ull;
     const uint32_t P = g.seg;
@@ -438,13 +502,13 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
         const uint32_t t = lane % P;
         const uint64_t sys = group * (64u / P) + lane / P;
         const bool live = sys < g.nsys && t < g.num_procs;
-        uint32_t w[4] = {0, 0, 0, 0};
+        uint32_t w[2] = {0, 0};
         if (live) {
             const uint64_t key =
                 fmix64(g.seed ^ ((g.sys_base + sys) * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull));
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k) {
-                const uint32_t i = chunk * 8 + k;
+            for (uint32_t k = 0; k < CHUNK; ++k) {
+                const uint32_t i = chunk * CHUNK + k;
                 if (i >= g.len) break;
                 const uint64_t r = fmix64(key ^ (((uint64_t)t << 32) | i) ^ 0x8CB92BA72F3D8DD7ull);
                 uint32_t value = (uint32_t)(r & 0xFF);
@@ -471,35 +535,46 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
             }
             if (chunk == 0) g.lens[sys * g.num_procs + t] = g.len;
         }
-        g.trace[gid] = make_uint4(w[0], w[1], w[2], w[3]);
+        g.trace[gid] = make_uint2(w[0], w[1]);
     }
 }
 
-template <int P, int CS>
-static hipError_t launch_sim_pc(const SimArgs& a, uint64_t groups, hipStream_t s) {
-    hipLaunchKernelGGL((sim_kernel<P, CS>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+template <int P, int CS, uint32_t RING>
+static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t s) {
+    hipLaunchKernelGGL((sim_kernel<P, CS, RING>), dim3((uint32_t)groups), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
-template <int P>
-static hipError_t launch_sim_p(const SimArgs& a, uint32_t cs, uint64_t groups, hipStream_t s) {
-    switch (cs) {
-    case 1: return launch_sim_pc<P, 1>(a, groups, s);
-    case 2: return launch_sim_pc<P, 2>(a, groups, s);
-    case 4: return launch_sim_pc<P, 4>(a, groups, s);
-    case 8: return launch_sim_pc<P, 8>(a, groups, s);
-    case 16: return launch_sim_pc<P, 16>(a, groups, s);
+template <int P, int CS>
+static hipError_t launch_sim_pc(const SimArgs& a, uint32_t ring, uint64_t groups, hipStream_t s) {
+    switch (ring) {
+    case 16: return launch_sim_pcr<P, CS, 16>(a, groups, s);
+    case 32: return launch_sim_pcr<P, CS, 32>(a, groups, s);
+    case 256: return launch_sim_pcr<P, CS, 256>(a, groups, s);
     default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint64_t groups, hipStream_t s) {
+template <int P>
+static hipError_t launch_sim_p(const SimArgs& a, uint32_t cs, uint32_t ring, uint64_t groups, hipStream_t s) {
+    switch (cs) {
+    case 1: return launch_sim_pc<P, 1>(a, ring, groups, s);
+    case 2: return launch_sim_pc<P, 2>(a, ring, groups, s);
+    case 4: return launch_sim_pc<P, 4>(a, ring, groups, s);
+    case 8: return launch_sim_pc<P, 8>(a, ring, groups, s);
+    case 16: return launch_sim_pc<P, 16>(a, ring, groups, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring, uint64_t groups,
+                      hipStream_t s) {
     if (groups == 0) return hipSuccess;
     switch (seg) {
-    case 1: return launch_sim_p<1>(a, cs, groups, s);
-    case 2: return launch_sim_p<2>(a, cs, groups, s);
-    case 4: return launch_sim_p<4>(a, cs, groups, s);
-    case 8: return launch_sim_p<8>(a, cs, groups, s);
+    case 1: return launch_sim_p<1>(a, cs, ring, groups, s);
+    case 2: return launch_sim_p<2>(a, cs, ring, groups, s);
+    case 4: return launch_sim_p<4>(a, cs, ring, groups, s);
+    case 8: return launch_sim_p<8>(a, cs, ring, groups, s);
     default: return hipErrorInvalidValue;
     }
 }

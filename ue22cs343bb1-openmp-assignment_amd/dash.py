@@ -39,6 +39,7 @@ TXN_NAMES = ("READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID"
 OK, EINVAL, EIO, EPARSE, EADDR, EDEVICE, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5, -6, -7
 ERR_OVERFLOW, ERR_OOB, ERR_CTZ0, ERR_DEADLOCK, ERR_ROUNDCAP = 1, 2, 4, 8, 16
 KEEP_STATE = 1
+TIER_FROM_32, TIER_FROM_256 = 2, 4
 GEN_UNIFORM, GEN_CONTENTION, GEN_LOCALITY = 0, 1, 2
 
 # every symbol include/dash.h declares
@@ -73,14 +74,16 @@ class Stats(ctypes.Structure):
                 ("rounds_total", ctypes.c_uint64), ("rounds_max", ctypes.c_uint64),
                 ("systems", ctypes.c_uint64), ("err_systems", ctypes.c_uint64),
                 ("err_bits", ctypes.c_uint64), ("dropped", ctypes.c_uint64),
-                ("max_depth", ctypes.c_uint64), ("kernel_ms", ctypes.c_double)]
+                ("max_depth", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
+                ("tier_systems", ctypes.c_uint64 * 3)]
 
     def as_dict(self):
         return {"hist": [int(x) for x in self.hist], "instructions": int(self.instructions),
                 "rounds_total": int(self.rounds_total), "rounds_max": int(self.rounds_max),
                 "systems": int(self.systems), "err_systems": int(self.err_systems),
                 "err_bits": int(self.err_bits), "dropped": int(self.dropped),
-                "max_depth": int(self.max_depth), "kernel_ms": float(self.kernel_ms)}
+                "max_depth": int(self.max_depth), "kernel_ms": float(self.kernel_ms),
+                "tier_systems": [int(x) for x in self.tier_systems]}
 
 
 class Gen(ctypes.Structure):
@@ -188,8 +191,8 @@ class Engine:
     """One batch of independent N-node systems on one GPU (a dash_t handle)."""
 
     def __init__(self, num_systems, num_procs=8, cache_size=4, max_instr=32, keep_state=False,
-                 device=0, max_rounds=0):
-        self.cfg = Cfg(num_procs, cache_size, max_instr, KEEP_STATE if keep_state else 0,
+                 device=0, max_rounds=0, flags=0):
+        self.cfg = Cfg(num_procs, cache_size, max_instr, (KEEP_STATE if keep_state else 0) | flags,
                        num_systems, max_rounds, device, 0)
         self.h = ctypes.c_void_p()
         _check(lib().dash_create(ctypes.byref(self.cfg), ctypes.byref(self.h)), "dash_create")

@@ -135,7 +135,7 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     chk(hipMalloc(&h->d_rounds, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(rounds)");
     chk(hipMalloc(&h->d_errors, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(errors)");
     chk(hipMalloc(&h->d_stats, dash::STAT_WORDS * sizeof(unsigned long long)), "hipMalloc(stats)");
-    chk(hipMalloc(&h->d_hist, std::max<uint64_t>(nsys * N, 1) * 13 * sizeof(uint32_t)), "hipMalloc(hist)");
+    chk(hipMalloc(&h->d_hist, std::max<uint64_t>(nsys, 1) * 13 * sizeof(uint32_t)), "hipMalloc(hist)");
     chk(hipMalloc(&h->d_list[0], std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(list)");
     chk(hipMalloc(&h->d_list[1], std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(list)");
     chk(hipMalloc(&h->d_count, 2 * sizeof(uint32_t)), "hipMalloc(count)");
@@ -228,7 +228,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
     a.rounds = h->d_rounds;
     a.errors = h->d_errors;
     a.state = h->d_state;
-    a.hist_node = h->d_hist;
+    a.hist = h->d_hist;
     a.keep = (h->cfg.flags & DASH_KEEP_STATE) ? 1u : 0u;
     a.stats = h->d_stats;
     const uint64_t spw = 64 / h->seg;
@@ -338,16 +338,10 @@ int dash_read_hist(dash_t* h, uint64_t sys, uint32_t* hist) {
     if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
     if (!(h->cfg.flags & DASH_KEEP_STATE)) return fail(h, DASH_ESTATE, "created without DASH_KEEP_STATE");
     if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
-    const uint32_t N = h->cfg.num_procs;
-    std::vector<uint32_t> w((size_t)N * 13);
     HIPCHK(h, hipSetDevice(h->cfg.device));
-    HIPCHK(h, hipMemcpyAsync(w.data(), h->d_hist + sys * N * 13, w.size() * 4, hipMemcpyDeviceToHost,
+    HIPCHK(h, hipMemcpyAsync(hist, h->d_hist + sys * 13, 13 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                              h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    for (int k = 0; k < 13; k++) {
-        hist[k] = 0;
-        for (uint32_t t = 0; t < N; t++) hist[k] += w[t * 13 + k];
-    }
     return DASH_OK;
 }
 

@@ -42,7 +42,7 @@ struct SimArgs {
     uint32_t* rounds;         // [sys]
     uint32_t* errors;         // [sys]
     uint32_t* state;          // optional [(sys*N+node)*(16+CS)] directory/cache words
-    uint32_t* hist_node;      // [(sys*N+node)*13]; written when keep or on counter drain
+    uint32_t* hist;           // [sys*13] messages handled per type; written when keep
     uint32_t keep;
     uint32_t _pad;
     unsigned long long* stats;  // [STAT_WORDS]

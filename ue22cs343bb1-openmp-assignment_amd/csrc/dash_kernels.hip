@@ -48,9 +48,8 @@ constexpr uint64_t TA_BASE = ((uint64_t)T_RID << (4 * T_UPG)) | ((uint64_t)T_FIA
                              ((uint64_t)T_FLUSH << (4 * T_WBINT)) | ((uint64_t)T_ES << (4 * T_ES)) |
                              ((uint64_t)T_RR << (4 * T_ISSUE_R)) | ((uint64_t)T_WRQ << (4 * T_ISSUE_W));
 
-constexpr uint32_t WIN = 3;        // trace window chunks per lane
+constexpr uint32_t WIN = 2;        // trace window chunks per lane (enough: see the refill)
 constexpr uint32_t CHUNK = 4;      // instructions per chunk (8 B)
-constexpr uint32_t HIST_FLUSH = 0x7FFF;  // u16 histogram counters drain every 32768 rounds
 
 // message word (ref `message`, :70-79, 20 B -> 4 B):
 //   [3:0] type  [6:4] sender  [15:8] address  [23:16] value | bitVector
@@ -69,96 +68,33 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
     return k;
 }
 
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp(uint32_t x) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
-}
-
-// ---- per-receiver counters packed FW bits per field (one field per node of the system) ----
-template <int P, int FW>
-struct Fields {
-    static constexpr int PER = 32 / FW;                  // fields per register
-    static constexpr int NR = (P + PER - 1) / PER;       // registers
-    static constexpr uint32_t LSB = FW == 8 ? 0x01010101u : 0x00010001u;
-    static constexpr uint32_t FMASK = (1u << FW) - 1u;
-    uint32_t r[NR];
-
-    __device__ __forceinline__ uint32_t get(uint32_t d) const {
-        uint32_t v = r[0];
-#pragma unroll
-        for (int k = 1; k < NR; ++k) v = (d / PER == (uint32_t)k) ? r[k] : v;
-        return (v >> (FW * (d % PER))) & FMASK;
-    }
-    // bits of `m` (bit i = node i) -> one in field i
-    __device__ __forceinline__ static Fields spread(uint32_t m) {
-        Fields f;
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            const uint32_t x = m >> (k * PER);
-            f.r[k] = FW == 8 ? (((x & 15u) * 0x00204081u) & 0x01010101u)
-                             : (((x & 3u) * 0x00008001u) & 0x00010001u);
-        }
-        return f;
-    }
-    __device__ __forceinline__ void add_one(bool v, uint32_t d) {
-        const uint32_t one = v ? (1u << (FW * (d % PER))) : 0u;
-#pragma unroll
-        for (int k = 0; k < NR; ++k) r[k] += (d / PER == (uint32_t)k) ? one : 0u;
-    }
-};
-
-// segmented (P lanes) exclusive prefix sum and total, on the VALU (DPP row
-// shifts, quad perms, half-row mirror): no LDS or permute traffic
-template <int P, int FW>
-__device__ __forceinline__ void seg_scan_total(const Fields<P, FW>& c, uint32_t t, Fields<P, FW>& ex,
-                                               Fields<P, FW>& tot) {
-#pragma unroll
-    for (int k = 0; k < Fields<P, FW>::NR; ++k) {
-        uint32_t il = c.r[k];
-        if constexpr (P >= 2) { const uint32_t y = dpp<0x111>(il); il += t >= 1 ? y : 0u; }  // row_shr:1
-        if constexpr (P >= 4) { const uint32_t y = dpp<0x112>(il); il += t >= 2 ? y : 0u; }  // row_shr:2
-        if constexpr (P >= 8) { const uint32_t y = dpp<0x114>(il); il += t >= 4 ? y : 0u; }  // row_shr:4
-        ex.r[k] = il - c.r[k];
-        uint32_t s = c.r[k];
-        if constexpr (P >= 2) s += dpp<0xB1>(s);   // quad_perm [1,0,3,2]
-        if constexpr (P >= 4) s += dpp<0x4E>(s);   // quad_perm [2,3,0,1]
-        if constexpr (P >= 8) s += dpp<0x141>(s);  // row_half_mirror
-        tot.r[k] = s;
-    }
-}
-
-// per field: min(x, RING); fields hold at most RING + 2P
-template <int FW, uint32_t RING>
-__device__ __forceinline__ uint32_t clamp_fields(uint32_t x) {
-    constexpr uint32_t TOP = 1u << (FW - 1);
-    constexpr uint32_t LSB = FW == 8 ? 0x01010101u : 0x00010001u;
-    constexpr uint32_t bias = (TOP - 1u - RING) * LSB;
-    const uint32_t over = ((x + bias) & (TOP * LSB)) >> (FW - 1);  // field > RING
-    const uint32_t m = (over << FW) - over;                        // field mask where over
-    return (x & ~m) | ((RING * LSB) & m);
-}
-
-template <int CS, uint32_t RING>
+template <int P, int CS, uint32_t RING>
 struct Lds {  // 32-bit word offsets
-    static constexpr uint32_t ENT = 0;                      // u16 [16][64]  mem | bitVector<<8
-    static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8
+    static constexpr uint32_t ENT = 0;                      // u16 [16][64]  mem | bitVector<<8   (swizzled)
+    static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8      (swizzled)
     static constexpr uint32_t RNG = CAC + CS * 64 / 2;      // u32 [RING][64] message words
-    static constexpr uint32_t WND = RNG + RING * 64;        // u16x4 [WIN][64] trace chunks
-    static constexpr uint32_t HST = WND + WIN * 64 * 2;     // u32 [7][64]   two u16 counters
-    static constexpr uint32_t WORDS = HST + 7 * 64;
+    static constexpr uint32_t WND = RNG + RING * 64;        // u32 [WIN][2][64] trace chunks (2 instr/word)
+    static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
+    static constexpr uint32_t HST = WND + WIN * 64 * 2;     // u32 [13][64/P+1] per-system counters
+    static constexpr uint32_t OUT = HST + 13 * HSTRIDE;     // u32 [2][64]   this round's sends
+    static constexpr uint32_t MSK = OUT + 2 * 64;           // u32 [64]      arrivals bitmask
+    static constexpr uint32_t DUM = MSK + 64;               // u32 [64]      scratch store target
+    static constexpr uint32_t WORDS = DUM + 64;
 };
 
 template <int P, int CS, uint32_t RING>
 __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
-    using L = Lds<CS, RING>;
-    constexpr int FW = RING <= 64 ? 8 : 16;
-    using F = Fields<P, FW>;
+    using L = Lds<P, CS, RING>;
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
     __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS];
     uint16_t* const lds16 = reinterpret_cast<uint16_t*>(lds);
 
     const uint32_t lane = threadIdx.x;
+    // u16 rows: lane l's half-word sits in dword (l & 31), half (l >> 5), so the 32
+    // lanes of each LDS lane group always touch 32 distinct banks whatever row each
+    // of them indexes
+    const uint32_t sw = ((lane & 31u) << 1) | (lane >> 5);
     const uint32_t t = lane & (P - 1);  // node id (threadId in the reference)
     const uint32_t seg = lane - t;
     const uint64_t slot_id = (uint64_t)blockIdx.x * SPW + lane / P;
@@ -174,16 +110,15 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     }
     uint32_t len = live ? a.lens[sys * N + t] : 0u;
     const uint32_t rcv_mask = (1u << N) - 1u;
-    uint32_t* const hist_row = a.hist_node + (sys * N + t) * 13;
 
     // initializeProcessor's state part (ref :808-820); directory/line states
     // live in two lane registers (2 bits per entry), the rest in LDS
 #pragma unroll
-    for (uint32_t b = 0; b < 16; ++b) lds16[L::ENT * 2 + b * 64 + lane] = (uint16_t)((20u * t + b) & 0xFFu);
+    for (uint32_t b = 0; b < 16; ++b) lds16[L::ENT * 2 + b * 64 + sw] = (uint16_t)((20u * t + b) & 0xFFu);
 #pragma unroll
-    for (uint32_t i = 0; i < CS; ++i) lds16[L::CAC * 2 + i * 64 + lane] = 0xFFu;
-#pragma unroll
-    for (uint32_t k = 0; k < 7; ++k) lds[L::HST + k * 64 + lane] = 0u;
+    for (uint32_t i = 0; i < CS; ++i) lds16[L::CAC * 2 + i * 64 + sw] = 0xFFu;
+    for (uint32_t w = lane; w < 13 * L::HSTRIDE; w += 64) lds[L::HST + w] = 0u;
+    lds[L::MSK + lane] = 0u;
     uint32_t dsv = 0xAAAAAAAAu;  // 16 x U
     uint32_t cst = 0xFFFFFFFFu;  // CS x INVALID
 
@@ -192,36 +127,33 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     const uint32_t nch = (len + CHUNK - 1) / CHUNK;
 #pragma unroll
     for (uint32_t c = 0; c < WIN; ++c)
-        if (c < nch) *reinterpret_cast<uint2*>(&lds[L::WND + (c * 64 + lane) * 2]) = tr[c * 64];
+        if (c < nch) {
+            const uint2 v = tr[c * 64];
+            lds[L::WND + (2 * c) * 64 + lane] = v.x;
+            lds[L::WND + (2 * c + 1) * 64 + lane] = v.y;
+        }
     uint32_t pend_idx = WIN;
     uint2 pend = make_uint2(0, 0);
     if (pend_idx < nch) pend = tr[pend_idx * 64];
 
-    // Every lane of a system carries the queue count and tail of ALL the
-    // system's nodes (one field per node, updated identically in every lane),
-    // so a sender finds its receiver's free slot without a cross-lane read.
-    F cnt, tail;
-#pragma unroll
-    for (int k = 0; k < F::NR; ++k) cnt.r[k] = tail.r[k] = 0u;
+    // this node's incoming queue (messageBuffer, ref :81-87): count and tail
+    // of an LDS ring; only the receiver touches them (arrivals are pulled)
+    uint32_t cnt = 0, tail = 0;
     uint32_t pc = 0, waiting = 0, last_val = 0;
     uint32_t err = 0, rounds = 0, maxd = 0, drops = 0;
-    bool flushed = false;
     const uint32_t cap = a.max_rounds;
     const bool final_tier = a.final_tier != 0;
 
     for (uint32_t r = 0;; ++r) {
         // ---- quiescence / round cap / tier overflow, on start-of-round state ----
-        uint32_t my_cnt = cnt.get(t);
         bool can_issue = !waiting && pc < len;
-        const uint64_t act = __ballot(my_cnt != 0 || can_issue);
+        const uint64_t act = __ballot(cnt != 0 || can_issue);
         if (act == 0) break;
         bool sys_act = ((uint32_t)(act >> seg) & SEGMASK) != 0;
         const bool sys_ovf = !final_tier && (((uint32_t)(__ballot((err & DASH_ERR_OVERFLOW_D) != 0) >> seg) & SEGMASK) != 0);
         if (sys_act && (rounds >= cap || sys_ovf)) {  // all lanes of a system agree
             err |= rounds >= cap ? DASH_ERR_ROUNDCAP_D : 0u;
-#pragma unroll
-            for (int k = 0; k < F::NR; ++k) cnt.r[k] = 0u;
-            my_cnt = 0;
+            cnt = 0;
             len = pc;
             waiting = 0;
             can_issue = false;
@@ -229,46 +161,36 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         }
         rounds += sys_act ? 1u : 0u;
 
-        // ---- wave-uniform housekeeping: trace window refill, histogram drain ----
+        // ---- wave-uniform housekeeping: trace window refill ----
+        // Invariant at a refill point: pend_idx >= pc/CHUNK + 1 and the window holds
+        // chunks pend_idx-2 and pend_idx-1. pc advances <= CHUNK per CHUNK rounds, so
+        // the chunks read until the next refill point (pc/CHUNK, pc/CHUNK + 1) are
+        // always resident; the pending chunk's load has CHUNK rounds to land.
         if ((r & (CHUNK - 1)) == 0) {
             if (pend_idx < nch && pend_idx < pc / CHUNK + WIN) {
-                *reinterpret_cast<uint2*>(&lds[L::WND + ((pend_idx % WIN) * 64 + lane) * 2]) = pend;
+                lds[L::WND + (2 * (pend_idx % WIN)) * 64 + lane] = pend.x;
+                lds[L::WND + (2 * (pend_idx % WIN) + 1) * 64 + lane] = pend.y;
                 ++pend_idx;
                 if (pend_idx < nch) pend = tr[pend_idx * 64];
-            }
-            if ((r & HIST_FLUSH) == HIST_FLUSH - (CHUNK - 1)) {
-#pragma unroll
-                for (uint32_t k = 0; k < 7; ++k) {
-                    const uint32_t w = lds[L::HST + k * 64 + lane];
-                    lds[L::HST + k * 64 + lane] = 0u;
-                    if (live) {
-                        hist_row[2 * k] = (flushed ? hist_row[2 * k] : 0u) + (w & 0xFFFFu);
-                        if (k < 6) hist_row[2 * k + 1] = (flushed ? hist_row[2 * k + 1] : 0u) + (w >> 16);
-                    }
-                }
-                flushed = true;
             }
         }
 
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
-        const bool has_msg = my_cnt != 0;
-        const uint32_t head = (tail.get(t) - my_cnt) & (RING - 1);
+        const bool has_msg = cnt != 0;
+        const uint32_t head = (tail - cnt) & (RING - 1);
         const uint32_t m = lds[L::RNG + head * 64 + lane];
-        const uint32_t ins = lds16[L::WND * 2 + (((pc / CHUNK) % WIN) * 64 + lane) * CHUNK + (pc & (CHUNK - 1))];
+        const uint32_t ins = lds16[(L::WND + (2 * ((pc / CHUNK) % WIN) + ((pc >> 1) & 1u)) * 64 + lane) * 2 + (pc & 1u)];
         const bool do_issue = !has_msg && can_issue;
         pc += do_issue ? 1u : 0u;
-        const F pops = F::spread((uint32_t)(__ballot(has_msg) >> seg) & SEGMASK);
-        F cp;  // queue counts after this round's pops
-#pragma unroll
-        for (int k = 0; k < F::NR; ++k) cp.r[k] = cnt.r[k] - pops.r[k];
+        cnt -= has_msg ? 1u : 0u;
 
         const uint32_t type = has_msg ? (m & 15u) : (do_issue ? (T_ISSUE_R + (ins >> 15)) : T_IDLE);
         const uint32_t addr = has_msg ? ((m >> 8) & 0xFFu) : ((ins >> 8) & 0x7Fu);
         const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         const uint32_t idx = b & (CS - 1);
-        const uint32_t e16 = lds16[L::ENT * 2 + b * 64 + lane];
-        const uint32_t c16 = lds16[L::CAC * 2 + idx * 64 + lane];
+        const uint32_t e16 = lds16[L::ENT * 2 + b * 64 + sw];
+        const uint32_t c16 = lds16[L::CAC * 2 + idx * 64 + sw];
 
         const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
         const uint32_t laddr = c16 & 0xFFu, lval = c16 >> 8, lst = (cst >> (2 * idx)) & 3u;
@@ -356,53 +278,66 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         err |= (oob ? DASH_ERR_OOB_D : 0u) | (ctz0 ? DASH_ERR_CTZ0_D : 0u);
         drops += (oob ? 1u : 0u) + (ctz0 ? 1u : 0u);
 
-        lds16[L::ENT * 2 + b * 64 + lane] = (uint16_t)(nmem | (nbv << 8));
-        lds16[L::CAC * 2 + idx * 64 + lane] = (uint16_t)(fill ? (addr | (fval << 8)) : c16);
+        lds16[L::ENT * 2 + b * 64 + sw] = (uint16_t)(nmem | (nbv << 8));
+        lds16[L::CAC * 2 + idx * 64 + sw] = (uint16_t)(fill ? (addr | (fval << 8)) : c16);
         dsv = (dsv & ~(3u << (2 * b))) | (nds << (2 * b));
         cst = (cst & ~(3u << (2 * idx))) | (nst << (2 * idx));
-        if (has_msg)
-            __hip_atomic_fetch_add(&lds[L::HST + ((m & 15u) >> 1) * 64 + lane], 1u << (16 * (m & 1u)),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (has_msg)  // messages handled per transactionType, per system
+            __hip_atomic_fetch_add(&lds[L::HST + (m & 15u) * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
 
         // ---- end-of-round delivery: lowest sender first, program order within a sender ----
-        F c = F::spread(inv), ex, tot;
-        c.add_one(vP, dP);
-        c.add_one(vB, dB);
-        seg_scan_total<P, FW>(c, t, ex, tot);
-        F sl, fl;  // per receiver: next free slot (tail + excl), fill level after earlier senders
-#pragma unroll
-        for (int k = 0; k < F::NR; ++k) {
-            sl.r[k] = tail.r[k] + ex.r[k];
-            fl.r[k] = cp.r[k] + ex.r[k];
-        }
-        auto deliver = [&](bool v, uint32_t d, uint32_t w, uint32_t local) {
-            const uint32_t slot = (sl.get(d) + local) & (RING - 1);
-            const bool ok = fl.get(d) + local < RING;
-            if (v & ok) lds[L::RNG + slot * 64 + seg + d] = w;
-            const bool dropped = v & !ok;
-            err |= dropped ? DASH_ERR_OVERFLOW_D : 0u;
-            drops += dropped ? 1u : 0u;
-        };
+        // A sender posts its words in the outbox and ORs bit 4*sender+k into each
+        // receiver's arrival mask, k = 0: INV, 1: primary, 2: flush copy (OR commutes:
+        // no ordering between lanes is needed); a receiver then appends its arrivals
+        // in ascending bit order = ascending sender, program order within a sender
+        // (the INVs precede the eviction notice, ref :364-379). Outbox slot 0 holds
+        // the primary word, slot 1 the flush copy or -- a REPLY_ID handler sends no
+        // flush copy -- the INV word.
+        lds[L::OUT + lane] = wP;
+        lds[L::OUT + 64 + lane] = inv ? mk(T_INV, t, addr, 0, 0, 0) : wA;
+        if (vP)
+            __hip_atomic_fetch_or(&lds[L::MSK + seg + dP], 2u << (4 * t), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (vB)
+            __hip_atomic_fetch_or(&lds[L::MSK + seg + dB], 4u << (4 * t), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         uint32_t im = inv;
-        if (__ballot(im != 0) != 0) {  // INVs precede the eviction notice (ref :364-379)
-            const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
+        if (__ballot(im != 0) != 0) {
             do {
-                const uint32_t j = (uint32_t)__builtin_ctz(im | 0x100u) & 7u;
-                deliver(im != 0, j, winv, 0u);
+                if (im != 0)
+                    __hip_atomic_fetch_or(&lds[L::MSK + seg + ((uint32_t)__builtin_ctz(im) & 7u)], 1u << (4 * t),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 im &= im - 1u;
             } while (__ballot(im != 0) != 0);
         }
-        deliver(vP, dP, wP, (inv >> dP) & 1u);
-        deliver(vB, dB, wA, (vA & (dP == dB)) ? 1u : 0u);
-
-        // every lane: new counts = min(count - pop + arrivals, RING); tails advance by delivered
-#pragma unroll
-        for (int k = 0; k < F::NR; ++k) {
-            const uint32_t n = clamp_fields<FW, RING>(cp.r[k] + tot.r[k]);
-            tail.r[k] = (tail.r[k] + (n - cp.r[k])) & ((RING - 1) * F::LSB);
-            cnt.r[k] = n;
+        uint32_t rm = __hip_atomic_exchange(&lds[L::MSK + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // two arrivals per trip: both outbox reads are in flight before the ring
+        // stores; a lane with nothing (left) to append stores to its scratch word.
+        // Bit 31 (sender 7, slot 3) is never posted, so ctz(rm | 1<<31) == 31 for
+        // an empty mask and its outbox read stays inside the LDS block.
+        while (__ballot(rm != 0) != 0) {
+            const uint32_t b0 = (uint32_t)__builtin_ctz(rm | 0x80000000u);
+            const uint32_t r1 = rm & (rm - 1u);
+            const uint32_t b1 = (uint32_t)__builtin_ctz(r1 | 0x80000000u);
+            const uint32_t w0 = lds[L::OUT + (~b0 & 1u) * 64 + seg + (b0 >> 2)];
+            const uint32_t w1 = lds[L::OUT + (~b1 & 1u) * 64 + seg + (b1 >> 2)];
+            const bool v0 = rm != 0, v1 = r1 != 0;
+            // sendMessage's capacity check (ref :754-761), per arrival in order
+            const bool ok0 = v0 & (cnt < RING);
+            const bool ok1 = v1 & (cnt + (ok0 ? 1u : 0u) < RING);
+            const uint32_t t1 = (tail + (ok0 ? 1u : 0u)) & (RING - 1);
+            lds[ok0 ? (L::RNG + tail * 64 + lane) : (L::DUM + lane)] = w0;
+            lds[ok1 ? (L::RNG + t1 * 64 + lane) : (L::DUM + lane)] = w1;
+            const uint32_t nok = (ok0 ? 1u : 0u) + (ok1 ? 1u : 0u);
+            const uint32_t nbad = ((v0 & !ok0) ? 1u : 0u) + ((v1 & !ok1) ? 1u : 0u);
+            tail = (tail + nok) & (RING - 1);
+            cnt += nok;
+            err |= nbad ? DASH_ERR_OVERFLOW_D : 0u;
+            drops += nbad;
+            rm = r1 & (r1 - 1u);
         }
-        maxd = max(maxd, cnt.get(t));
+        maxd = max(maxd, cnt);
     }
 
     // ---- results ----
@@ -414,18 +349,14 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     const bool handoff = !final_tier && (serr & DASH_ERR_OVERFLOW_D) != 0;
     const bool report = live && !handoff;
 
-    uint32_t hcnt[13];
+    uint32_t hcnt[13];  // this system's per-type counts (read by its node-0 lane)
 #pragma unroll
-    for (uint32_t k = 0; k < 7; ++k) {
-        const uint32_t w = lds[L::HST + k * 64 + lane];
-        hcnt[2 * k] = (w & 0xFFFFu) + ((flushed && live) ? hist_row[2 * k] : 0u);
-        if (k < 6) hcnt[2 * k + 1] = (w >> 16) + ((flushed && live) ? hist_row[2 * k + 1] : 0u);
-    }
+    for (uint32_t k = 0; k < 13; ++k) hcnt[k] = lds[L::HST + k * L::HSTRIDE + lane / P];
     uint64_t h = 0x243F6A8885A308D3ull ^ ((uint64_t)t << 56);
     for (uint32_t b = 0; b < 16; ++b)
-        h = fmix64(h ^ (uint64_t)(lds16[L::ENT * 2 + b * 64 + lane] | (((dsv >> (2 * b)) & 3u) << 16)));
+        h = fmix64(h ^ (uint64_t)(lds16[L::ENT * 2 + b * 64 + sw] | (((dsv >> (2 * b)) & 3u) << 16)));
     for (uint32_t i = 0; i < CS; ++i)
-        h = fmix64(h ^ ((uint64_t)(lds16[L::CAC * 2 + i * 64 + lane] | (((cst >> (2 * i)) & 3u) << 16)) |
+        h = fmix64(h ^ ((uint64_t)(lds16[L::CAC * 2 + i * 64 + sw] | (((cst >> (2 * i)) & 3u) << 16)) |
                         (1ull << 24)));
     uint64_t dg = 0x9E3779B97F4A7C15ull;
 #pragma unroll
@@ -442,12 +373,12 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     if (a.state && report) {
         uint32_t* st = a.state + (sys * N + t) * (16 + CS);
         for (uint32_t b = 0; b < 16; ++b)
-            st[b] = lds16[L::ENT * 2 + b * 64 + lane] | (((dsv >> (2 * b)) & 3u) << 16);
+            st[b] = lds16[L::ENT * 2 + b * 64 + sw] | (((dsv >> (2 * b)) & 3u) << 16);
         for (uint32_t i = 0; i < CS; ++i)
-            st[16 + i] = lds16[L::CAC * 2 + i * 64 + lane] | (((cst >> (2 * i)) & 3u) << 16);
+            st[16 + i] = lds16[L::CAC * 2 + i * 64 + sw] | (((cst >> (2 * i)) & 3u) << 16);
     }
-    if (report && (a.keep || flushed))
-        for (uint32_t k = 0; k < 13; ++k) hist_row[k] = hcnt[k];
+    if (report && t == 0 && a.keep)
+        for (uint32_t k = 0; k < 13; ++k) a.hist[sys * 13 + k] = hcnt[k];
 
     // ---- global statistics: wave reductions, one atomic per counter per wave ----
     const bool head_lane = report && t == 0;
@@ -464,7 +395,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         return v;
     };
     for (uint32_t k = 0; k < 13; ++k) {
-        const uint64_t v = wsum(report ? hcnt[k] : 0u);
+        const uint64_t v = wsum(head_lane ? hcnt[k] : 0u);
         if (lane == 0 && v) atomicAdd(&S[STAT_HIST + k], (unsigned long long)v);
     }
     const uint64_t s_instr = wsum(report ? pc : 0u);

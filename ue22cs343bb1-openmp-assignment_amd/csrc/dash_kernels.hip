@@ -41,10 +41,12 @@ enum : uint32_t { D_EM = 0, D_S = 1, D_U = 2 };              // directoryEntrySt
 
 #define B(x) (1u << (x))
 constexpr uint32_t M_CLRW = B(T_RRD) | B(T_RWR) | B(T_RID) | B(T_FLUSH) | B(T_FIA);
-// default outgoing type per handled type (nibble per type): UPGRADE->REPLY_ID,
+// default outgoing type per handled type (nibble per type): READ_REQUEST->REPLY_RD,
+// WRITE_REQUEST->REPLY_ID (both corrected by directory state), UPGRADE->REPLY_ID,
 // WRITEBACK_INV->FLUSH_INVACK, WRITEBACK_INT->FLUSH, EVICT_SHARED->EVICT_SHARED,
-// RD miss->READ_REQUEST, WR miss->WRITE_REQUEST; READ/WRITE_REQUEST resolved by dir state
-constexpr uint64_t TA_BASE = ((uint64_t)T_RID << (4 * T_UPG)) | ((uint64_t)T_FIA << (4 * T_WBINV)) |
+// RD miss->READ_REQUEST, WR miss->WRITE_REQUEST (corrected to UPGRADE on a hit)
+constexpr uint64_t TA_BASE = ((uint64_t)T_RRD << (4 * T_RR)) | ((uint64_t)T_RID << (4 * T_WRQ)) |
+                             ((uint64_t)T_RID << (4 * T_UPG)) | ((uint64_t)T_FIA << (4 * T_WBINV)) |
                              ((uint64_t)T_FLUSH << (4 * T_WBINT)) | ((uint64_t)T_ES << (4 * T_ES)) |
                              ((uint64_t)T_RR << (4 * T_ISSUE_R)) | ((uint64_t)T_WRQ << (4 * T_ISSUE_W));
 
@@ -76,11 +78,17 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t WND = RNG + RING * 64;        // u32 [WIN][2][64] trace chunks (2 instr/word)
     static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
     static constexpr uint32_t HST = WND + WIN * 64 * 2;     // u32 [13][64/P+1] per-system counters
-    static constexpr uint32_t OUT = HST + 13 * HSTRIDE;     // u32 [2][64]   this round's sends
-    static constexpr uint32_t MSK = OUT + 2 * 64;           // u32 [64]      arrivals bitmask
-    static constexpr uint32_t DUM = MSK + 64;               // u32 [64]      scratch store target
+    static constexpr uint32_t MQ = (HST + 13 * HSTRIDE + 1) & ~1u;  // u32 [64][2] arrivals mask, tail|count<<16
+    static constexpr uint32_t DUM = MQ + 2 * 64;            // u32 [64]      target of a suppressed store
     static constexpr uint32_t WORDS = DUM + 64;
 };
+
+// 0 / ~0 mask: bit `i` of the constant set `s` (one v_bfe_i32 with an SGPR constant)
+__device__ __forceinline__ uint32_t bit_mask(uint32_t s, uint32_t i) {
+    return (uint32_t)__builtin_amdgcn_sbfe((int)s, i, 1);
+}
+__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+__device__ __forceinline__ uint32_t mask_of(bool c) { return c ? ~0u : 0u; }
 
 template <int P, int CS, uint32_t RING>
 __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
@@ -97,6 +105,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     const uint32_t sw = ((lane & 31u) << 1) | (lane >> 5);
     const uint32_t t = lane & (P - 1);  // node id (threadId in the reference)
     const uint32_t seg = lane - t;
+    const uint32_t tbit = 1u << t;
     const uint64_t slot_id = (uint64_t)blockIdx.x * SPW + lane / P;
     const uint32_t N = a.num_procs;
     bool live;
@@ -118,7 +127,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
 #pragma unroll
     for (uint32_t i = 0; i < CS; ++i) lds16[L::CAC * 2 + i * 64 + sw] = 0xFFu;
     for (uint32_t w = lane; w < 13 * L::HSTRIDE; w += 64) lds[L::HST + w] = 0u;
-    lds[L::MSK + lane] = 0u;
+    lds[L::MQ + 2 * lane] = 0u;
     uint32_t dsv = 0xAAAAAAAAu;  // 16 x U
     uint32_t cst = 0xFFFFFFFFu;  // CS x INVALID
 
@@ -136,30 +145,33 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     uint2 pend = make_uint2(0, 0);
     if (pend_idx < nch) pend = tr[pend_idx * 64];
 
-    // this node's incoming queue (messageBuffer, ref :81-87): count and tail
-    // of an LDS ring; only the receiver touches them (arrivals are pulled)
+    // this node's incoming queue (messageBuffer, ref :81-87): count and tail of
+    // its LDS ring, owned by the node; senders learn them through MQ each round
     uint32_t cnt = 0, tail = 0;
     uint32_t pc = 0, waiting = 0, last_val = 0;
-    uint32_t err = 0, rounds = 0, maxd = 0, drops = 0;
+    uint32_t err = 0, maxd = 0, drops = 0;
+    uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
     const uint32_t cap = a.max_rounds;
-    const bool final_tier = a.final_tier != 0;
 
     for (uint32_t r = 0;; ++r) {
-        // ---- quiescence / round cap / tier overflow, on start-of-round state ----
-        bool can_issue = !waiting && pc < len;
-        const uint64_t act = __ballot(cnt != 0 || can_issue);
+        // ---- quiescence / round cap, on start-of-round state ----
+        // A system is active while any of its nodes has a message or can issue;
+        // quiescence is absorbing, so the active rounds of a system are 0..R-1.
+        bool can_issue = (waiting == 0) & (pc < len);
+        bool active = (cnt != 0) | can_issue;
+        const uint64_t act = __ballot(active);
         if (act == 0) break;
-        bool sys_act = ((uint32_t)(act >> seg) & SEGMASK) != 0;
-        const bool sys_ovf = !final_tier && (((uint32_t)(__ballot((err & DASH_ERR_OVERFLOW_D) != 0) >> seg) & SEGMASK) != 0);
-        if (sys_act && (rounds >= cap || sys_ovf)) {  // all lanes of a system agree
-            err |= rounds >= cap ? DASH_ERR_ROUNDCAP_D : 0u;
-            cnt = 0;
-            len = pc;
-            waiting = 0;
-            can_issue = false;
-            sys_act = false;
+        if (r == cap) {  // wave-uniform: every system still active has run `cap` rounds
+            if (((uint32_t)(act >> seg) & SEGMASK) != 0) {
+                err |= DASH_ERR_ROUNDCAP_D;
+                cnt = 0;
+                len = pc;
+                waiting = 0;
+                can_issue = false;
+                active = false;
+            }
         }
-        rounds += sys_act ? 1u : 0u;
+        last_act = active ? r : last_act;
 
         // ---- wave-uniform housekeeping: trace window refill ----
         // Invariant at a refill point: pend_idx >= pc/CHUNK + 1 and the window holds
@@ -177,176 +189,183 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
 
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
         const bool has_msg = cnt != 0;
-        const uint32_t head = (tail - cnt) & (RING - 1);
-        const uint32_t m = lds[L::RNG + head * 64 + lane];
+        const uint32_t m = lds[L::RNG + ((tail - cnt) & (RING - 1)) * 64 + lane];
         const uint32_t ins = lds16[(L::WND + (2 * ((pc / CHUNK) % WIN) + ((pc >> 1) & 1u)) * 64 + lane) * 2 + (pc & 1u)];
-        const bool do_issue = !has_msg && can_issue;
+        const bool do_issue = !has_msg & can_issue;
         pc += do_issue ? 1u : 0u;
         cnt -= has_msg ? 1u : 0u;
-
-        const uint32_t type = has_msg ? (m & 15u) : (do_issue ? (T_ISSUE_R + (ins >> 15)) : T_IDLE);
-        const uint32_t addr = has_msg ? ((m >> 8) & 0xFFu) : ((ins >> 8) & 0x7Fu);
+        // an issued instruction is pseudo-type 13 (RD) / 14 (WR) with its address in
+        // the message address field; an idle node is type 15
+        const uint32_t mw = has_msg ? m : ((ins & 0x7F00u) | (do_issue ? (T_ISSUE_R + (ins >> 15)) : T_IDLE));
+        const uint32_t ty = mw & 15u;
+        const uint32_t addr = (mw >> 8) & 0xFFu;
         const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         const uint32_t idx = b & (CS - 1);
         const uint32_t e16 = lds16[L::ENT * 2 + b * 64 + sw];
         const uint32_t c16 = lds16[L::CAC * 2 + idx * 64 + sw];
+        if (has_msg)  // messages handled per transactionType, per system
+            __hip_atomic_fetch_add(&lds[L::HST + ty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
 
         const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
         const uint32_t laddr = c16 & 0xFFu, lval = c16 >> 8, lst = (cst >> (2 * idx)) & 3u;
-        const uint32_t msender = (m >> 4) & 7u, mval = (m >> 16) & 0xFFu;
-        const uint32_t msr = (m >> 24) & 7u, mds_s = (m >> 27) & 1u;
+        const uint32_t msender = (mw >> 4) & 7u, mval = (mw >> 16) & 0xFFu;
+        const uint32_t msr = (mw >> 24) & 7u, mds_s = (mw >> 27) & 1u;
         const uint32_t ival = ins & 0xFFu;
         const uint32_t sbit = 1u << msender;
 
         // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
-        // one-hot type; every predicate below is bitwise so the step stays branch-free
-        const uint32_t tb = 1u << type;
-        auto any = [&](uint32_t mask) { return (tb & mask) != 0u; };
-        const bool tH = t == H, tSR = t == msr;
-        const bool dsEM = ds == D_EM, dsS = ds == D_S, dsU = ds == D_U;
-        const bool same = laddr == addr;
-        const bool hit = same & (lst != ST_I);              // ref :662-664
-        const bool own_hit = any(B(T_ISSUE_W)) & hit & (lst != ST_S);  // WR hit on M/E (:706-710)
-        const uint32_t es_bv = bv & ~sbit;                  // also UPGRADE/WRITE_REQUEST's sharer list
-        const uint32_t es_pop = (uint32_t)__builtin_popcount(es_bv);
+        // every predicate is a 0/~0 VGPR mask: type sets are one bit-extract of a
+        // constant, states one bit-extract of a one-hot constant, selects bitwise
+#define TS(set) bit_mask((set), ty)
+        const uint32_t dsEM = bit_mask(1u << D_EM, ds), dsS = bit_mask(1u << D_S, ds), dsU = bit_mask(1u << D_U, ds);
+        const uint32_t lI = bit_mask(1u << ST_I, lst), lS = bit_mask(1u << ST_S, lst);
+        const uint32_t mTH = bit_mask(tbit, H), mTSR = bit_mask(tbit, msr);
+        const uint32_t same = mask_of(laddr == addr);
+        const uint32_t hit = same & ~lI;                                   // ref :662-664
+        const uint32_t own_hit = TS(B(T_ISSUE_W)) & hit & ~lS;             // WR hit on M/E (:706-710)
+        const uint32_t es_bv = bv & ~sbit;           // also UPGRADE/WRITE_REQUEST's sharer list
+        const uint32_t es_one = mask_of(__builtin_popcount(es_bv) == 1u);
+        const uint32_t es_none = mask_of(es_bv == 0u);
         const uint32_t es_own = (uint32_t)__builtin_ctz(es_bv | 0x100u);
-        const bool esH = any(B(T_ES)) & tH;
-        const bool es_one = esH & (es_pop == 1u);
-        const bool em_req = any(B(T_RR) | B(T_WRQ)) & dsEM;
-        const bool ctz0 = em_req & (bv == 0u);              // ref UB (:209, :451): drop + flag
-        const bool homeH = tH & any(B(T_FLUSH) | B(T_FIA));
+        const uint32_t esH = TS(B(T_ES)) & mTH;
+        const uint32_t req = TS(B(T_RR) | B(T_WRQ));
+        const uint32_t em_req = req & dsEM;
+        const uint32_t ctz0 = em_req & mask_of(bv == 0u);                 // ref UB (:209, :451): drop + flag
+        const uint32_t homeH = TS(B(T_FLUSH) | B(T_FIA)) & mTH;
 
-        // directory entry + memory
-        const bool to_req = (any(B(T_RR)) & dsU) | any(B(T_WRQ) | B(T_UPG));  // :234 :456 :346
-        uint32_t nbv = (any(B(T_RR)) & dsS) ? (bv | sbit) : bv;                // :222
-        nbv = to_req ? sbit : nbv;
-        nbv = homeH ? ((any(B(T_FLUSH)) ? bv : 0u) | (1u << msr)) : nbv;       // :304 :517
-        nbv = esH ? es_bv : nbv;                                               // :561
-        nbv = any(B(T_EMOD)) ? 0u : nbv;                                       // :615
-        uint32_t nds = to_req ? (uint32_t)D_EM : ds;
-        nds = (homeH & any(B(T_FLUSH))) ? (uint32_t)D_S : nds;                  // :303
-        nds = esH ? (es_pop == 0u ? (uint32_t)D_U : (es_pop == 1u ? (uint32_t)D_EM : ds)) : nds;
-        nds = any(B(T_EMOD)) ? (uint32_t)D_U : nds;                             // :616
-        const uint32_t nmem = (homeH | any(B(T_EMOD))) ? mval : mem;           // :307 :520 :602
+        // directory entry + memory (ref :222,234 :304,517 :346,456 :561 :615)
+        const uint32_t to_req = (TS(B(T_RR)) & dsU) | TS(B(T_WRQ) | B(T_UPG));
+        const uint32_t bv_set = (((TS(B(T_RR)) & dsS) | to_req) & sbit) | (homeH & (1u << msr));
+        const uint32_t bv_clr = to_req | TS(B(T_EMOD)) | (TS(B(T_FIA)) & mTH) | (esH & sbit);
+        const uint32_t nbv = (bv & ~bv_clr) | bv_set;
+        const uint32_t nds_em = to_req | (esH & es_one);
+        const uint32_t nds_s = TS(B(T_FLUSH)) & mTH;
+        const uint32_t nds_u = TS(B(T_EMOD)) | (esH & es_none);
+        const uint32_t nds = (ds & ~(nds_em | nds_s | nds_u)) | (nds_s & D_S) | (nds_u & D_U);
+        const uint32_t nmem = sel(homeH | TS(B(T_EMOD)), mval, mem);  // :307 :520 :602
 
         // cache line
-        const bool fill = any(B(T_RRD) | B(T_RWR) | B(T_RID)) | (any(B(T_FLUSH) | B(T_FIA)) & tSR) | own_hit;
-        const uint32_t fval = any(B(T_RRD) | B(T_FLUSH)) ? mval : (any(B(T_ISSUE_W)) ? ival : last_val);
-        const uint32_t fst = any(B(T_RRD)) ? (mds_s ? ST_S : ST_E) : (any(B(T_FLUSH)) ? ST_S : ST_M);
-        uint32_t nst = ((any(B(T_INV)) & same) | any(B(T_WBINV))) ? ST_I : lst;  // :396-398 :501
-        nst = any(B(T_WBINT)) ? ST_S : nst;                                    // :284
-        nst = (any(B(T_ES)) & (!tH | (es_one & (es_own == H)))) ? ST_E : nst;  // :558 :586
-        nst = fill ? fst : nst;
+        const uint32_t fill = TS(B(T_RRD) | B(T_RWR) | B(T_RID)) | (TS(B(T_FLUSH) | B(T_FIA)) & mTSR) | own_hit;
+        const uint32_t fval = sel(TS(B(T_RRD) | B(T_FLUSH)), mval, sel(TS(B(T_ISSUE_W)), ival, last_val));
+        const uint32_t fst = (TS(B(T_FLUSH)) & ST_S) | (TS(B(T_RRD)) & (ST_E + mds_s));
+        uint32_t nst = sel((TS(B(T_INV)) & same) | TS(B(T_WBINV)), ST_I, lst);     // :396-398 :501
+        nst = sel(TS(B(T_WBINT)), ST_S, nst);                                     // :284
+        const uint32_t own_home = mask_of(es_own == H);
+        nst = sel(TS(B(T_ES)) & (~mTH | (es_one & own_home)), ST_E, nst);         // :558 :586
+        nst = sel(fill, fst, nst);
         // handleCacheReplacement of the refilled line (:767-804); REPLY_WR unconditional (:467)
-        const bool ev = fill & (lst != ST_I) & (any(B(T_RWR)) | !same);
+        const uint32_t ev = fill & ~lI & (TS(B(T_RWR)) | ~same);
 
         // primary outgoing message: the handler's reply/forward, or else the eviction
         // notice -- no handler sends both (fills never reply), so one slot serves both
-        const bool vA = (any(B(T_RR) | B(T_WRQ)) & !ctz0) | any(B(T_UPG) | B(T_WBINV) | B(T_WBINT)) |
-                        (es_one & (es_own != H)) | (any(B(T_ISSUE_R) | B(T_ISSUE_W)) & !hit) |
-                        (any(B(T_ISSUE_W)) & hit & !own_hit);
-        uint32_t dA = any(B(T_RR) | B(T_WRQ) | B(T_UPG)) ? msender : H;
-        dA = em_req ? (uint32_t)__builtin_ctz(bv | 0x100u) : dA;
-        dA = esH ? es_own : dA;
-        // reply type per request type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453)
-        uint32_t tA = (uint32_t)((TA_BASE >> (4 * type)) & 15u);
-        tA = any(B(T_RR)) ? (dsEM ? T_WBINT : T_RRD) : tA;
-        tA = any(B(T_WRQ)) ? (dsEM ? T_WBINV : (dsU ? T_RWR : T_RID)) : tA;
-        tA = (any(B(T_ISSUE_W)) & hit) ? T_UPG : tA;
-        uint32_t valA = any(B(T_WBINV) | B(T_WBINT)) ? lval : mem;
-        valA = any(B(T_ISSUE_W)) ? ival : valA;
-        valA = (any(B(T_UPG)) | (any(B(T_WRQ)) & !dsEM)) ? es_bv : valA;
-        valA = (any(B(T_WRQ)) & dsEM) ? mval : valA;
-        const uint32_t srA = any(B(T_WBINV) | B(T_WBINT)) ? msr : msender;
-        const uint32_t wA = mk(tA, t, addr, valA, srA, dsS ? 1u : 0u);
+        const uint32_t issue = TS(B(T_ISSUE_R) | B(T_ISSUE_W));
+        const uint32_t vA = (req & ~ctz0) | TS(B(T_UPG) | B(T_WBINV) | B(T_WBINT)) | (esH & es_one & ~own_home) |
+                            (TS(B(T_ISSUE_R)) & ~hit) | (TS(B(T_ISSUE_W)) & ~own_hit);
+        uint32_t dA = sel(req | TS(B(T_UPG)), msender, H);
+        dA = sel(em_req, (uint32_t)__builtin_ctz(bv | 0x100u), dA);
+        dA = sel(esH, es_own, dA);
+        // reply type: the per-type default, then READ_REQUEST (ref :199-236) and
+        // WRITE_REQUEST (:417-453) by directory state, and UPGRADE for a WR hit
+        uint32_t tA = (uint32_t)((TA_BASE >> (4 * ty)) & 15u);
+        tA += (TS(B(T_RR)) & dsEM & (T_WBINT - T_RRD)) + (TS(B(T_WRQ)) & dsEM & (T_WBINV - T_RID)) +
+              (TS(B(T_ISSUE_W)) & hit & (T_UPG - T_WRQ));
+        tA -= TS(B(T_WRQ)) & dsU & (T_RID - T_RWR);
+        uint32_t valA = sel(TS(B(T_WBINV) | B(T_WBINT)), lval, mem);
+        valA = sel(issue, ival, valA);
+        valA = sel(TS(B(T_UPG)) | (TS(B(T_WRQ)) & ~dsEM), es_bv, valA);
+        valA = sel(TS(B(T_WRQ)) & dsEM, mval, valA);
+        const uint32_t srA = sel(TS(B(T_WBINV) | B(T_WBINT)), msr, msender);
+        const uint32_t wA = mk(tA, t, addr, valA, srA, 0) | (dsS & (1u << 27));
         const uint32_t dE = laddr >> 4;
-        const bool vE = ev & (dE < N);
-        const uint32_t wE = mk(lst == ST_M ? T_EMOD : T_ES, t, laddr, lval, 0, 0);
-        const bool vP = vA | vE;
-        const uint32_t dP = (vA ? dA : dE) & 7u;
-        const uint32_t wP = vA ? wA : wE;
+        const uint32_t inN = mask_of(dE < N);
+        const uint32_t vE = ev & inN;
+        const uint32_t wE = (lst == ST_M ? T_EMOD : T_ES) | (t << 4) | (c16 << 8);
+        const bool vP = (vA | vE) != 0;
+        const uint32_t dP = sel(vA, dA, dE) & 7u;
+        const uint32_t wP = sel(vA, wA, wE);
         // second copy of a flush: WRITEBACK_INV always (:498), WRITEBACK_INT if sr != home (:281)
-        const bool vB = any(B(T_WBINV)) | (any(B(T_WBINT)) & (H != msr));
-        const uint32_t dB = msr;
-        const uint32_t inv = any(B(T_RID)) ? (mval & rcv_mask) : 0u;  // REPLY_ID fan-out (:364-373)
+        const bool vB = (TS(B(T_WBINV)) | (TS(B(T_WBINT)) & mask_of(H != msr))) != 0;
+        const uint32_t inv = TS(B(T_RID)) & mval & rcv_mask;  // REPLY_ID fan-out (:364-373)
 
-        waiting = (any(B(T_ISSUE_R) | B(T_ISSUE_W)) & !own_hit & !(any(B(T_ISSUE_R)) & hit))
-                      ? 1u : (any(M_CLRW) ? 0u : waiting);
-        last_val = any(B(T_ISSUE_R)) ? 0u : (any(B(T_ISSUE_W)) ? ival : last_val);
-        const bool oob = ev & (dE >= N);  // ref UB: messageBuffers[15] -> drop + flag
-        err |= (oob ? DASH_ERR_OOB_D : 0u) | (ctz0 ? DASH_ERR_CTZ0_D : 0u);
-        drops += (oob ? 1u : 0u) + (ctz0 ? 1u : 0u);
+        const uint32_t wset = (TS(B(T_ISSUE_R)) & ~hit) | (TS(B(T_ISSUE_W)) & ~own_hit);
+        waiting = (waiting & ~TS(M_CLRW)) | (wset & 1u);
+        last_val = sel(issue, ival, last_val);
+        const uint32_t oob = ev & ~inN;  // ref UB: messageBuffers[15] -> drop + flag
+        err |= (oob & DASH_ERR_OOB_D) | (ctz0 & DASH_ERR_CTZ0_D);
+        drops += (oob & 1u) + (ctz0 & 1u);
+#undef TS
 
         lds16[L::ENT * 2 + b * 64 + sw] = (uint16_t)(nmem | (nbv << 8));
-        lds16[L::CAC * 2 + idx * 64 + sw] = (uint16_t)(fill ? (addr | (fval << 8)) : c16);
+        lds16[L::CAC * 2 + idx * 64 + sw] = (uint16_t)sel(fill, addr | (fval << 8), c16);
         dsv = (dsv & ~(3u << (2 * b))) | (nds << (2 * b));
         cst = (cst & ~(3u << (2 * idx))) | (nst << (2 * idx));
-        if (has_msg)  // messages handled per transactionType, per system
-            __hip_atomic_fetch_add(&lds[L::HST + (m & 15u) * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
 
         // ---- end-of-round delivery: lowest sender first, program order within a sender ----
-        // A sender posts its words in the outbox and ORs bit 4*sender+k into each
-        // receiver's arrival mask, k = 0: INV, 1: primary, 2: flush copy (OR commutes:
-        // no ordering between lanes is needed); a receiver then appends its arrivals
-        // in ascending bit order = ascending sender, program order within a sender
-        // (the INVs precede the eviction notice, ref :364-379). Outbox slot 0 holds
-        // the primary word, slot 1 the flush copy or -- a REPLY_ID handler sends no
-        // flush copy -- the INV word.
-        lds[L::OUT + lane] = wP;
-        lds[L::OUT + 64 + lane] = inv ? mk(T_INV, t, addr, 0, 0, 0) : wA;
+        // Each node publishes its queue tail and count (after this round's pop);
+        // a sender ORs bit 4*sender+k into its receiver's arrival mask, k = 0: INV,
+        // 1: primary, 2: flush copy (OR commutes: no ordering between lanes). The
+        // arrivals' queue order is then ascending bit order = ascending sender,
+        // program order within a sender (the INVs precede the eviction notice,
+        // ref :364-379): a sender's slot is the receiver's tail plus the number of
+        // bits below its own, and the receiver's capacity check (ref :754-761)
+        // compares the receiver's count plus that rank with the ring depth.
+        lds[L::MQ + 2 * lane + 1] = tail | (cnt << 16);
+        const uint32_t bitP = 2u << (4 * t), bitB = 4u << (4 * t), bitI = 1u << (4 * t);
         if (vP)
-            __hip_atomic_fetch_or(&lds[L::MSK + seg + dP], 2u << (4 * t), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (vB)
-            __hip_atomic_fetch_or(&lds[L::MSK + seg + dB], 4u << (4 * t), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-        uint32_t im = inv;
-        if (__ballot(im != 0) != 0) {
+            __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const bool any_inv = __ballot(inv != 0) != 0;
+        if (any_inv) {
+            uint32_t im = inv;
             do {
                 if (im != 0)
-                    __hip_atomic_fetch_or(&lds[L::MSK + seg + ((uint32_t)__builtin_ctz(im) & 7u)], 1u << (4 * t),
+                    __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + ((uint32_t)__builtin_ctz(im) & 7u))], bitI,
                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 im &= im - 1u;
             } while (__ballot(im != 0) != 0);
         }
-        uint32_t rm = __hip_atomic_exchange(&lds[L::MSK + lane], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // two arrivals per trip: both outbox reads are in flight before the ring
-        // stores; a lane with nothing (left) to append stores to its scratch word.
-        // Bit 31 (sender 7, slot 3) is never posted, so ctz(rm | 1<<31) == 31 for
-        // an empty mask and its outbox read stays inside the LDS block.
-        while (__ballot(rm != 0) != 0) {
-            const uint32_t b0 = (uint32_t)__builtin_ctz(rm | 0x80000000u);
-            const uint32_t r1 = rm & (rm - 1u);
-            const uint32_t b1 = (uint32_t)__builtin_ctz(r1 | 0x80000000u);
-            const uint32_t w0 = lds[L::OUT + (~b0 & 1u) * 64 + seg + (b0 >> 2)];
-            const uint32_t w1 = lds[L::OUT + (~b1 & 1u) * 64 + seg + (b1 >> 2)];
-            const bool v0 = rm != 0, v1 = r1 != 0;
-            // sendMessage's capacity check (ref :754-761), per arrival in order
-            const bool ok0 = v0 & (cnt < RING);
-            const bool ok1 = v1 & (cnt + (ok0 ? 1u : 0u) < RING);
-            const uint32_t t1 = (tail + (ok0 ? 1u : 0u)) & (RING - 1);
-            lds[ok0 ? (L::RNG + tail * 64 + lane) : (L::DUM + lane)] = w0;
-            lds[ok1 ? (L::RNG + t1 * 64 + lane) : (L::DUM + lane)] = w1;
-            const uint32_t nok = (ok0 ? 1u : 0u) + (ok1 ? 1u : 0u);
-            const uint32_t nbad = ((v0 & !ok0) ? 1u : 0u) + ((v1 & !ok1) ? 1u : 0u);
-            tail = (tail + nok) & (RING - 1);
-            cnt += nok;
-            err |= nbad ? DASH_ERR_OVERFLOW_D : 0u;
-            drops += nbad;
-            rm = r1 & (r1 - 1u);
+        auto place = [&](bool v, uint32_t d, uint32_t bit, uint32_t w) {
+            const uint2 q = *reinterpret_cast<const uint2*>(&lds[L::MQ + 2 * (seg + d)]);
+            const uint32_t rank = (uint32_t)__builtin_popcount(q.x & (bit - 1u));
+            const bool ok = v & (((q.y >> 16) + rank) < RING);
+            const uint32_t slot = ((q.y & 0xFFFFu) + rank) & (RING - 1);
+            lds[ok ? (L::RNG + slot * 64 + seg + d) : (L::DUM + lane)] = w;
+            const bool lost = v & !ok;
+            err |= lost ? DASH_ERR_OVERFLOW_D : 0u;
+            drops += lost ? 1u : 0u;
+        };
+        place(vP, dP, bitP, wP);
+        place(vB, msr, bitB, wA);
+        if (any_inv) {
+            const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
+            uint32_t im = inv;
+            do {
+                place(im != 0, (uint32_t)__builtin_ctz(im | 0x100u) & 7u, bitI, winv);
+                im &= im - 1u;
+            } while (__ballot(im != 0) != 0);
         }
+        const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQ + 2 * lane], 0u, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t n = min((uint32_t)__builtin_popcount(arrived), RING - cnt);
+        tail = (tail + n) & (RING - 1);
+        cnt += n;
         maxd = max(maxd, cnt);
     }
 
     // ---- results ----
     if (waiting) err |= DASH_ERR_DEADLOCK_D;
     uint32_t serr = err;
+    uint32_t rounds = last_act + 1u;  // ~0 + 1 = 0 for a system that never ran
 #pragma unroll
-    for (uint32_t n = 1; n < P; n <<= 1) serr |= __shfl_xor(serr, n, P);
+    for (uint32_t n = 1; n < P; n <<= 1) {
+        serr |= __shfl_xor(serr, n, P);
+        rounds = max(rounds, (uint32_t)__shfl_xor(rounds, n, P));
+    }
     // a non-final tier hands overflowed systems to the next tier: no outputs, no statistics
-    const bool handoff = !final_tier && (serr & DASH_ERR_OVERFLOW_D) != 0;
+    const bool handoff = a.final_tier == 0 && (serr & DASH_ERR_OVERFLOW_D) != 0;
     const bool report = live && !handoff;
 
     uint32_t hcnt[13];  // this system's per-type counts (read by its node-0 lane)

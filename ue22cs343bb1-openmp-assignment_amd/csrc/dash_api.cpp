@@ -33,7 +33,8 @@ struct dash_ctx {
     unsigned long long* d_stats = nullptr;
     uint32_t* d_list[2] = {nullptr, nullptr};  // overflow hand-off lists (ping-pong)
     uint32_t* d_count = nullptr;
-    uint64_t tier_systems[3] = {0, 0, 0};      // systems run per queue-depth tier, last run
+    uint64_t tier_systems[dash::NUM_TIERS] = {};  // systems run per queue-depth tier, last run
+    int auto_tier = 0;                         // adaptive first tier
     bool loaded = false;
     bool ran = false;
     char msg[256] = {0};
@@ -237,31 +238,39 @@ int dash_run(dash_t* h, dash_stats* stats) {
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     // queue-depth tiers: every system runs at the first depth; systems that would
     // overflow it are listed and re-run from scratch at the next depth (exact:
-    // the lockstep schedule is deterministic); the last tier drops like the reference
+    // the lockstep schedule is deterministic); the last tier drops like the reference.
+    // Without a DASH_TIER_FROM_* flag the first depth adapts: when more than 1/32 of
+    // the systems overflowed the first depth of a run, later runs start one deeper.
     uint64_t todo = h->cfg.num_systems;
     const uint32_t* list = nullptr;
-    const int first = (h->cfg.flags & DASH_TIER_FROM_256) ? 2 : (h->cfg.flags & DASH_TIER_FROM_32) ? 1 : 0;
-    for (int tier = 0; tier < 3; ++tier) h->tier_systems[tier] = 0;
-    for (int tier = first; tier < 3; ++tier) {
+    const uint32_t f = h->cfg.flags;
+    const int first = (f & DASH_TIER_FROM_256) ? 3 : (f & DASH_TIER_FROM_32) ? 2 : (f & DASH_TIER_FROM_16) ? 1
+                                                                                                   : h->auto_tier;
+    for (int tier = 0; tier < dash::NUM_TIERS; ++tier) h->tier_systems[tier] = 0;
+    for (int tier = first; tier < dash::NUM_TIERS; ++tier) {
+        const bool last = tier == dash::NUM_TIERS - 1;
         h->tier_systems[tier] = todo;
         if (todo == 0) continue;
         uint32_t* out = h->d_list[tier & 1];
         uint32_t* cnt = h->d_count + (tier & 1);
         a.sys_list = list;
         a.list_len = todo;
-        a.final_tier = tier == 2 ? 1u : 0u;
+        a.final_tier = last ? 1u : 0u;
         a.ovf_list = out;
         a.ovf_count = cnt;
         HIPCHK(h, hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
         HIPCHK(h, dash::launch_sim(a, h->seg, h->cfg.cache_size, dash::RING_TIERS[tier], (todo + spw - 1) / spw,
                                    h->stream));
-        if (tier == 2) break;
+        if (last) break;
         uint32_t next = 0;
         HIPCHK(h, hipMemcpyAsync(&next, cnt, sizeof next, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         todo = next;
         list = out;
     }
+    if (!(f & (DASH_TIER_FROM_16 | DASH_TIER_FROM_32 | DASH_TIER_FROM_256)) && first < dash::NUM_TIERS - 1 &&
+        h->tier_systems[first + 1] * 32 > h->tier_systems[first])
+        h->auto_tier = first + 1;
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     unsigned long long s[dash::STAT_WORDS];
     HIPCHK(h, hipMemcpyAsync(s, h->d_stats, sizeof s, hipMemcpyDeviceToHost, h->stream));
@@ -281,7 +290,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
         stats->dropped = s[dash::STAT_DROPS];
         stats->max_depth = s[dash::STAT_MAXDEPTH];
         stats->kernel_ms = ms;
-        for (int k = 0; k < 3; k++) stats->tier_systems[k] = h->tier_systems[k];
+        for (int k = 0; k < dash::NUM_TIERS; k++) stats->tier_systems[k] = h->tier_systems[k];
     }
     return DASH_OK;
 }

@@ -39,17 +39,6 @@ enum : uint32_t {
 enum : uint32_t { ST_M = 0, ST_E = 1, ST_S = 2, ST_I = 3 };  // cacheLineState (ref :17)
 enum : uint32_t { D_EM = 0, D_S = 1, D_U = 2 };              // directoryEntryState (ref :28)
 
-#define B(x) (1u << (x))
-constexpr uint32_t M_CLRW = B(T_RRD) | B(T_RWR) | B(T_RID) | B(T_FLUSH) | B(T_FIA);
-// default outgoing type per handled type (nibble per type): READ_REQUEST->REPLY_RD,
-// WRITE_REQUEST->REPLY_ID (both corrected by directory state), UPGRADE->REPLY_ID,
-// WRITEBACK_INV->FLUSH_INVACK, WRITEBACK_INT->FLUSH, EVICT_SHARED->EVICT_SHARED,
-// RD miss->READ_REQUEST, WR miss->WRITE_REQUEST (corrected to UPGRADE on a hit)
-constexpr uint64_t TA_BASE = ((uint64_t)T_RRD << (4 * T_RR)) | ((uint64_t)T_RID << (4 * T_WRQ)) |
-                             ((uint64_t)T_RID << (4 * T_UPG)) | ((uint64_t)T_FIA << (4 * T_WBINV)) |
-                             ((uint64_t)T_FLUSH << (4 * T_WBINT)) | ((uint64_t)T_ES << (4 * T_ES)) |
-                             ((uint64_t)T_RR << (4 * T_ISSUE_R)) | ((uint64_t)T_WRQ << (4 * T_ISSUE_W));
-
 constexpr uint32_t WIN = 2;        // trace window chunks per lane (enough: see the refill)
 constexpr uint32_t CHUNK = 4;      // instructions per chunk (8 B)
 
@@ -75,20 +64,20 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t ENT = 0;                      // u16 [16][64]  mem | bitVector<<8   (swizzled)
     static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8      (swizzled)
     static constexpr uint32_t RNG = CAC + CS * 64 / 2;      // u32 [RING][64] message words
-    static constexpr uint32_t WND = RNG + RING * 64;        // u32 [WIN][2][64] trace chunks (2 instr/word)
+    static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*CHUNK][64] trace window  (swizzled)
     static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
-    static constexpr uint32_t HST = WND + WIN * 64 * 2;     // u32 [13][64/P+1] per-system counters
+    static constexpr uint32_t HST = WND + WIN * CHUNK * 64 / 2;  // u32 [13][64/P+1] per-system counters
     static constexpr uint32_t MQ = (HST + 13 * HSTRIDE + 1) & ~1u;  // u32 [64][2] arrivals mask, tail|count<<16
     static constexpr uint32_t DUM = MQ + 2 * 64;            // u32 [64]      target of a suppressed store
     static constexpr uint32_t WORDS = DUM + 64;
 };
 
-// 0 / ~0 mask: bit `i` of the constant set `s` (one v_bfe_i32 with an SGPR constant)
-__device__ __forceinline__ uint32_t bit_mask(uint32_t s, uint32_t i) {
-    return (uint32_t)__builtin_amdgcn_sbfe((int)s, i, 1);
+// ring index arithmetic for any depth R (x < 2R)
+template <uint32_t R>
+__device__ __forceinline__ uint32_t wrap(uint32_t x) {
+    if constexpr ((R & (R - 1)) == 0) return x & (R - 1);
+    else return x >= R ? x - R : x;
 }
-__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
-__device__ __forceinline__ uint32_t mask_of(bool c) { return c ? ~0u : 0u; }
 
 template <int P, int CS, uint32_t RING>
 __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
@@ -105,7 +94,6 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     const uint32_t sw = ((lane & 31u) << 1) | (lane >> 5);
     const uint32_t t = lane & (P - 1);  // node id (threadId in the reference)
     const uint32_t seg = lane - t;
-    const uint32_t tbit = 1u << t;
     const uint64_t slot_id = (uint64_t)blockIdx.x * SPW + lane / P;
     const uint32_t N = a.num_procs;
     bool live;
@@ -134,13 +122,17 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     // trace window prefill: chunks 0..WIN-1 landed, chunk WIN pending in registers
     const uint2* tr = a.trace + ((sys / SPW) * a.nchunks) * 64 + (sys % SPW) * P + t;
     const uint32_t nch = (len + CHUNK - 1) / CHUNK;
+    // instruction i of a lane lives in window row i % (WIN*CHUNK)
+    auto put_chunk = [&](uint32_t c, uint2 v) {
+        uint16_t* const w = lds16 + L::WND * 2 + ((c % WIN) * CHUNK) * 64 + sw;
+        w[0] = (uint16_t)v.x;
+        w[64] = (uint16_t)(v.x >> 16);
+        w[128] = (uint16_t)v.y;
+        w[192] = (uint16_t)(v.y >> 16);
+    };
 #pragma unroll
     for (uint32_t c = 0; c < WIN; ++c)
-        if (c < nch) {
-            const uint2 v = tr[c * 64];
-            lds[L::WND + (2 * c) * 64 + lane] = v.x;
-            lds[L::WND + (2 * c + 1) * 64 + lane] = v.y;
-        }
+        if (c < nch) put_chunk(c, tr[c * 64]);
     uint32_t pend_idx = WIN;
     uint2 pend = make_uint2(0, 0);
     if (pend_idx < nch) pend = tr[pend_idx * 64];
@@ -179,9 +171,18 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         // the chunks read until the next refill point (pc/CHUNK, pc/CHUNK + 1) are
         // always resident; the pending chunk's load has CHUNK rounds to land.
         if ((r & (CHUNK - 1)) == 0) {
+            // a non-final tier stops a system soon after its first overflow: it will be
+            // re-simulated from scratch at the next depth, its results here are void
+            if (a.final_tier == 0) {
+                const uint64_t ovf = __ballot((err & DASH_ERR_OVERFLOW_D) != 0);
+                if (ovf != 0 && ((uint32_t)(ovf >> seg) & SEGMASK) != 0) {
+                    cnt = 0;
+                    len = pc;
+                    waiting = 0;
+                }
+            }
             if (pend_idx < nch && pend_idx < pc / CHUNK + WIN) {
-                lds[L::WND + (2 * (pend_idx % WIN)) * 64 + lane] = pend.x;
-                lds[L::WND + (2 * (pend_idx % WIN) + 1) * 64 + lane] = pend.y;
+                put_chunk(pend_idx, pend);
                 ++pend_idx;
                 if (pend_idx < nch) pend = tr[pend_idx * 64];
             }
@@ -189,116 +190,128 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
 
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
         const bool has_msg = cnt != 0;
-        const uint32_t m = lds[L::RNG + ((tail - cnt) & (RING - 1)) * 64 + lane];
-        const uint32_t ins = lds16[(L::WND + (2 * ((pc / CHUNK) % WIN) + ((pc >> 1) & 1u)) * 64 + lane) * 2 + (pc & 1u)];
+        const uint32_t m = lds[L::RNG + wrap<RING>(tail + RING - cnt) * 64 + lane];
+        const uint32_t ins = lds16[L::WND * 2 + (pc % (WIN * CHUNK)) * 64 + sw];
         const bool do_issue = !has_msg & can_issue;
         pc += do_issue ? 1u : 0u;
         cnt -= has_msg ? 1u : 0u;
-        // an issued instruction is pseudo-type 13 (RD) / 14 (WR) with its address in
-        // the message address field; an idle node is type 15
-        const uint32_t mw = has_msg ? m : ((ins & 0x7F00u) | (do_issue ? (T_ISSUE_R + (ins >> 15)) : T_IDLE));
-        const uint32_t ty = mw & 15u;
-        const uint32_t addr = (mw >> 8) & 0xFFu;
+        // message addresses are < 0x80 (a send to a node >= N is dropped), so bits
+        // 14..8 give the address of a message and of an instruction alike
+        const uint32_t mw = has_msg ? m : ins;
+        const uint32_t addr = (mw >> 8) & 0x7Fu;
         const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         const uint32_t idx = b & (CS - 1);
         const uint32_t e16 = lds16[L::ENT * 2 + b * 64 + sw];
         const uint32_t c16 = lds16[L::CAC * 2 + idx * 64 + sw];
+        const uint32_t mty = m & 15u;
         if (has_msg)  // messages handled per transactionType, per system
-            __hip_atomic_fetch_add(&lds[L::HST + ty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
+            __hip_atomic_fetch_add(&lds[L::HST + mty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+
+        // The kernel is VALU-issue bound: predicates are lane masks
+        // (one v_cmp each), combined by the scalar unit, consumed by v_cndmask.
+        const bool isW = (ins & 0x8000u) != 0;
+        const bool iR = do_issue & !isW, iW = do_issue & isW;
+        const bool RR = has_msg & (mty == T_RR), WRQ = has_msg & (mty == T_WRQ);
+        const bool RRD = has_msg & (mty == T_RRD), RWR = has_msg & (mty == T_RWR);
+        const bool RID = has_msg & (mty == T_RID), INV = has_msg & (mty == T_INV);
+        const bool UPG = has_msg & (mty == T_UPG), WBINV = has_msg & (mty == T_WBINV);
+        const bool WBINT = has_msg & (mty == T_WBINT), FLUSH = has_msg & (mty == T_FLUSH);
+        const bool FIA = has_msg & (mty == T_FIA), ES = has_msg & (mty == T_ES);
+        const bool EMOD = has_msg & (mty == T_EMOD);
 
         const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
         const uint32_t laddr = c16 & 0xFFu, lval = c16 >> 8, lst = (cst >> (2 * idx)) & 3u;
-        const uint32_t msender = (mw >> 4) & 7u, mval = (mw >> 16) & 0xFFu;
-        const uint32_t msr = (mw >> 24) & 7u, mds_s = (mw >> 27) & 1u;
+        const uint32_t msender = (m >> 4) & 7u, mval = (mw >> 16) & 0xFFu;
+        const uint32_t msr = (m >> 24) & 7u;
+        const bool mds_s = (m & (1u << 27)) != 0;
         const uint32_t ival = ins & 0xFFu;
         const uint32_t sbit = 1u << msender;
 
         // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
-        // every predicate is a 0/~0 VGPR mask: type sets are one bit-extract of a
-        // constant, states one bit-extract of a one-hot constant, selects bitwise
-#define TS(set) bit_mask((set), ty)
-        const uint32_t dsEM = bit_mask(1u << D_EM, ds), dsS = bit_mask(1u << D_S, ds), dsU = bit_mask(1u << D_U, ds);
-        const uint32_t lI = bit_mask(1u << ST_I, lst), lS = bit_mask(1u << ST_S, lst);
-        const uint32_t mTH = bit_mask(tbit, H), mTSR = bit_mask(tbit, msr);
-        const uint32_t same = mask_of(laddr == addr);
-        const uint32_t hit = same & ~lI;                                   // ref :662-664
-        const uint32_t own_hit = TS(B(T_ISSUE_W)) & hit & ~lS;             // WR hit on M/E (:706-710)
-        const uint32_t es_bv = bv & ~sbit;           // also UPGRADE/WRITE_REQUEST's sharer list
-        const uint32_t es_one = mask_of(__builtin_popcount(es_bv) == 1u);
-        const uint32_t es_none = mask_of(es_bv == 0u);
-        const uint32_t es_own = (uint32_t)__builtin_ctz(es_bv | 0x100u);
-        const uint32_t esH = TS(B(T_ES)) & mTH;
-        const uint32_t req = TS(B(T_RR) | B(T_WRQ));
-        const uint32_t em_req = req & dsEM;
-        const uint32_t ctz0 = em_req & mask_of(bv == 0u);                 // ref UB (:209, :451): drop + flag
-        const uint32_t homeH = TS(B(T_FLUSH) | B(T_FIA)) & mTH;
+        const bool dsEM = ds == D_EM, dsS = ds == D_S, dsU = !dsEM & !dsS;
+        const bool lI = lst == ST_I, lS = lst == ST_S;
+        const bool tH = t == H, tSR = t == msr;
+        const bool same = laddr == addr;
+        const bool hit = same & !lI;                     // ref :662-664
+        const bool own_hit = iW & hit & !lS;             // WR hit on M/E (:706-710)
+        const uint32_t es_bv = bv & ~sbit;               // also UPGRADE/WRITE_REQUEST's sharer list
+        const uint32_t es_pop = (uint32_t)__builtin_popcount(es_bv);
+        const uint32_t es_own = (uint32_t)__builtin_ctz(es_bv | 0x100u);  // meaningful when es_pop == 1
+        const bool esH = ES & tH;
+        const bool es_one = esH & (es_pop == 1u);
+        const bool req = RR | WRQ;
+        const bool em_req = req & dsEM;
+        const bool ctz0 = em_req & (bv == 0u);           // ref UB (:209, :451): drop + flag
+        const bool homeH = (FLUSH | FIA) & tH;
 
         // directory entry + memory (ref :222,234 :304,517 :346,456 :561 :615)
-        const uint32_t to_req = (TS(B(T_RR)) & dsU) | TS(B(T_WRQ) | B(T_UPG));
-        const uint32_t bv_set = (((TS(B(T_RR)) & dsS) | to_req) & sbit) | (homeH & (1u << msr));
-        const uint32_t bv_clr = to_req | TS(B(T_EMOD)) | (TS(B(T_FIA)) & mTH) | (esH & sbit);
-        const uint32_t nbv = (bv & ~bv_clr) | bv_set;
-        const uint32_t nds_em = to_req | (esH & es_one);
-        const uint32_t nds_s = TS(B(T_FLUSH)) & mTH;
-        const uint32_t nds_u = TS(B(T_EMOD)) | (esH & es_none);
-        const uint32_t nds = (ds & ~(nds_em | nds_s | nds_u)) | (nds_s & D_S) | (nds_u & D_U);
-        const uint32_t nmem = sel(homeH | TS(B(T_EMOD)), mval, mem);  // :307 :520 :602
+        const bool to_req = (RR & dsU) | WRQ | UPG;
+        uint32_t nbv = (RR & dsS) ? (bv | sbit) : bv;
+        nbv = to_req ? sbit : nbv;
+        nbv = homeH ? ((FIA ? 0u : bv) | (1u << msr)) : nbv;
+        nbv = esH ? es_bv : nbv;
+        nbv = EMOD ? 0u : nbv;
+        uint32_t nds = (to_req | (es_one)) ? (uint32_t)D_EM : ds;
+        nds = (FLUSH & tH) ? (uint32_t)D_S : nds;
+        nds = (EMOD | (esH & (es_pop == 0u))) ? (uint32_t)D_U : nds;
+        const uint32_t nmem = (homeH | EMOD) ? mval : mem;  // :307 :520 :602
 
         // cache line
-        const uint32_t fill = TS(B(T_RRD) | B(T_RWR) | B(T_RID)) | (TS(B(T_FLUSH) | B(T_FIA)) & mTSR) | own_hit;
-        const uint32_t fval = sel(TS(B(T_RRD) | B(T_FLUSH)), mval, sel(TS(B(T_ISSUE_W)), ival, last_val));
-        const uint32_t fst = (TS(B(T_FLUSH)) & ST_S) | (TS(B(T_RRD)) & (ST_E + mds_s));
-        uint32_t nst = sel((TS(B(T_INV)) & same) | TS(B(T_WBINV)), ST_I, lst);     // :396-398 :501
-        nst = sel(TS(B(T_WBINT)), ST_S, nst);                                     // :284
-        const uint32_t own_home = mask_of(es_own == H);
-        nst = sel(TS(B(T_ES)) & (~mTH | (es_one & own_home)), ST_E, nst);         // :558 :586
-        nst = sel(fill, fst, nst);
+        const bool fill = RRD | RWR | RID | ((FLUSH | FIA) & tSR) | own_hit;
+        const uint32_t fval = (RRD | FLUSH) ? mval : (iW ? ival : last_val);
+        const uint32_t fst = RRD ? (mds_s ? ST_S : ST_E) : (FLUSH ? ST_S : ST_M);
+        const bool own_home = es_own == H;
+        uint32_t nst = ((INV & same) | WBINV) ? ST_I : lst;               // :396-398 :501
+        nst = WBINT ? ST_S : nst;                                         // :284
+        nst = (ES & (!tH | (es_one & own_home))) ? ST_E : nst;            // :558 :586
+        nst = fill ? fst : nst;
         // handleCacheReplacement of the refilled line (:767-804); REPLY_WR unconditional (:467)
-        const uint32_t ev = fill & ~lI & (TS(B(T_RWR)) | ~same);
+        const bool ev = fill & !lI & (RWR | !same);
 
         // primary outgoing message: the handler's reply/forward, or else the eviction
         // notice -- no handler sends both (fills never reply), so one slot serves both
-        const uint32_t issue = TS(B(T_ISSUE_R) | B(T_ISSUE_W));
-        const uint32_t vA = (req & ~ctz0) | TS(B(T_UPG) | B(T_WBINV) | B(T_WBINT)) | (esH & es_one & ~own_home) |
-                            (TS(B(T_ISSUE_R)) & ~hit) | (TS(B(T_ISSUE_W)) & ~own_hit);
-        uint32_t dA = sel(req | TS(B(T_UPG)), msender, H);
-        dA = sel(em_req, (uint32_t)__builtin_ctz(bv | 0x100u), dA);
-        dA = sel(esH, es_own, dA);
-        // reply type: the per-type default, then READ_REQUEST (ref :199-236) and
-        // WRITE_REQUEST (:417-453) by directory state, and UPGRADE for a WR hit
-        uint32_t tA = (uint32_t)((TA_BASE >> (4 * ty)) & 15u);
-        tA += (TS(B(T_RR)) & dsEM & (T_WBINT - T_RRD)) + (TS(B(T_WRQ)) & dsEM & (T_WBINV - T_RID)) +
-              (TS(B(T_ISSUE_W)) & hit & (T_UPG - T_WRQ));
-        tA -= TS(B(T_WRQ)) & dsU & (T_RID - T_RWR);
-        uint32_t valA = sel(TS(B(T_WBINV) | B(T_WBINT)), lval, mem);
-        valA = sel(issue, ival, valA);
-        valA = sel(TS(B(T_UPG)) | (TS(B(T_WRQ)) & ~dsEM), es_bv, valA);
-        valA = sel(TS(B(T_WRQ)) & dsEM, mval, valA);
-        const uint32_t srA = sel(TS(B(T_WBINV) | B(T_WBINT)), msr, msender);
-        const uint32_t wA = mk(tA, t, addr, valA, srA, 0) | (dsS & (1u << 27));
+        const bool vA = (req & !ctz0) | UPG | WBINV | WBINT | (es_one & !own_home) | (iR & !hit) | (iW & !own_hit);
+        uint32_t dA = (req | UPG) ? msender : H;
+        dA = em_req ? (uint32_t)__builtin_ctz(bv | 0x100u) : dA;
+        dA = esH ? es_own : dA;
+        // reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue: :666-734)
+        uint32_t tA = iR ? (uint32_t)T_RR : (uint32_t)T_WRQ;
+        tA = (iW & hit) ? (uint32_t)T_UPG : tA;
+        tA = UPG ? (uint32_t)T_RID : tA;
+        tA = WBINV ? (uint32_t)T_FIA : tA;
+        tA = WBINT ? (uint32_t)T_FLUSH : tA;
+        tA = ES ? (uint32_t)T_ES : tA;
+        tA = RR ? (dsEM ? (uint32_t)T_WBINT : (uint32_t)T_RRD) : tA;
+        tA = WRQ ? (dsEM ? (uint32_t)T_WBINV : (dsU ? (uint32_t)T_RWR : (uint32_t)T_RID)) : tA;
+        uint32_t valA = (WBINV | WBINT) ? lval : mem;
+        valA = do_issue ? ival : valA;
+        valA = (UPG | (WRQ & !dsEM)) ? es_bv : valA;
+        valA = (WRQ & dsEM) ? mval : valA;
+        const uint32_t srA = (WBINV | WBINT) ? msr : msender;
+        const uint32_t wA = mk(tA, t, addr, valA, srA, dsS ? 1u : 0u);
         const uint32_t dE = laddr >> 4;
-        const uint32_t inN = mask_of(dE < N);
-        const uint32_t vE = ev & inN;
-        const uint32_t wE = (lst == ST_M ? T_EMOD : T_ES) | (t << 4) | (c16 << 8);
-        const bool vP = (vA | vE) != 0;
-        const uint32_t dP = sel(vA, dA, dE) & 7u;
-        const uint32_t wP = sel(vA, wA, wE);
+        const bool inN = dE < N;
+        const bool vE = ev & inN;
+        const uint32_t wE = (lst == ST_M ? (uint32_t)T_EMOD : (uint32_t)T_ES) | (t << 4) | (c16 << 8);
+        const bool vP = vA | vE;
+        const uint32_t dP = (vA ? dA : dE) & 7u;
+        const uint32_t wP = vA ? wA : wE;
         // second copy of a flush: WRITEBACK_INV always (:498), WRITEBACK_INT if sr != home (:281)
-        const bool vB = (TS(B(T_WBINV)) | (TS(B(T_WBINT)) & mask_of(H != msr))) != 0;
-        const uint32_t inv = TS(B(T_RID)) & mval & rcv_mask;  // REPLY_ID fan-out (:364-373)
+        const bool vB = WBINV | (WBINT & (H != msr));
+        const uint32_t inv = RID ? (mval & rcv_mask) : 0u;  // REPLY_ID fan-out (:364-373)
 
-        const uint32_t wset = (TS(B(T_ISSUE_R)) & ~hit) | (TS(B(T_ISSUE_W)) & ~own_hit);
-        waiting = (waiting & ~TS(M_CLRW)) | (wset & 1u);
-        last_val = sel(issue, ival, last_val);
-        const uint32_t oob = ev & ~inN;  // ref UB: messageBuffers[15] -> drop + flag
-        err |= (oob & DASH_ERR_OOB_D) | (ctz0 & DASH_ERR_CTZ0_D);
-        drops += (oob & 1u) + (ctz0 & 1u);
-#undef TS
+        waiting = ((iR & !hit) | (iW & !own_hit)) ? 1u : ((RRD | RWR | RID | FLUSH | FIA) ? 0u : waiting);
+        last_val = do_issue ? ival : last_val;
+        const bool oob = ev & !inN;  // ref UB: messageBuffers[15] -> drop + flag
+        if (__ballot(oob | ctz0) != 0) {  // rare: keep the counting off the common path
+            err |= (oob ? DASH_ERR_OOB_D : 0u) | (ctz0 ? DASH_ERR_CTZ0_D : 0u);
+            drops += (oob ? 1u : 0u) + (ctz0 ? 1u : 0u);
+        }
 
         lds16[L::ENT * 2 + b * 64 + sw] = (uint16_t)(nmem | (nbv << 8));
-        lds16[L::CAC * 2 + idx * 64 + sw] = (uint16_t)sel(fill, addr | (fval << 8), c16);
+        lds16[L::CAC * 2 + idx * 64 + sw] = (uint16_t)(fill ? (addr | (fval << 8)) : c16);
         dsv = (dsv & ~(3u << (2 * b))) | (nds << (2 * b));
         cst = (cst & ~(3u << (2 * idx))) | (nst << (2 * idx));
 
@@ -331,7 +344,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
             const uint2 q = *reinterpret_cast<const uint2*>(&lds[L::MQ + 2 * (seg + d)]);
             const uint32_t rank = (uint32_t)__builtin_popcount(q.x & (bit - 1u));
             const bool ok = v & (((q.y >> 16) + rank) < RING);
-            const uint32_t slot = ((q.y & 0xFFFFu) + rank) & (RING - 1);
+            const uint32_t slot = wrap<RING>((q.y & 0xFFFFu) + rank);  // used only when ok
             lds[ok ? (L::RNG + slot * 64 + seg + d) : (L::DUM + lane)] = w;
             const bool lost = v & !ok;
             err |= lost ? DASH_ERR_OVERFLOW_D : 0u;
@@ -350,7 +363,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQ + 2 * lane], 0u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         const uint32_t n = min((uint32_t)__builtin_popcount(arrived), RING - cnt);
-        tail = (tail + n) & (RING - 1);
+        tail = wrap<RING>(tail + n);
         cnt += n;
         maxd = max(maxd, cnt);
     }
@@ -498,6 +511,7 @@ static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t 
 template <int P, int CS>
 static hipError_t launch_sim_pc(const SimArgs& a, uint32_t ring, uint64_t groups, hipStream_t s) {
     switch (ring) {
+    case 12: return launch_sim_pcr<P, CS, 12>(a, groups, s);
     case 16: return launch_sim_pcr<P, CS, 16>(a, groups, s);
     case 32: return launch_sim_pcr<P, CS, 32>(a, groups, s);
     case 256: return launch_sim_pcr<P, CS, 256>(a, groups, s);

@@ -100,8 +100,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--first-depth", type=int, choices=[0, 16, 32, 256], default=0,
-                    help="first queue-depth tier (0 = adaptive, starting at 12)")
+    ap.add_argument("--first-depth", type=int, choices=[0, 32, 256], default=0,
+                    help="first queue-depth tier (0 = adaptive, starting at 16)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -120,7 +120,7 @@ def main():
             "locality": dash.GEN_LOCALITY}[args.kind]
     locality = int(round(args.locality * 65536)) if args.kind == "locality" else 0
     M = args.systems
-    tier_flag = {0: 0, 16: dash.TIER_FROM_16, 32: dash.TIER_FROM_32, 256: dash.TIER_FROM_256}[args.first_depth]
+    tier_flag = {0: 0, 32: dash.TIER_FROM_32, 256: dash.TIER_FROM_256}[args.first_depth]
     eng = dash.Engine(M, num_procs=8, cache_size=args.cache_size, max_instr=args.len,
                       device=local_rank, flags=tier_flag)
     sys_base, M = shard(rank, world, M)

@@ -38,8 +38,8 @@ extern "C" {
 #define DASH_MAX_CACHE 16
 #define DASH_RING_DEPTH 256 /* per-node queue capacity = ref MSG_BUFFER_SIZE (:9); the engine
                               runs shallower LDS queues first and re-runs, from scratch, any
-                              system that would fill one (12 -> 16 -> 32 -> 256) */
-#define DASH_NUM_TIERS 4
+                              system that would fill one (16 -> 32 -> 256) */
+#define DASH_NUM_TIERS 3
 #define DASH_NUM_TXN 13    /* transactionType (ref :30-44) */
 
 /* return codes */
@@ -69,9 +69,8 @@ enum dash_txn {
 /* flags */
 #define DASH_KEEP_STATE 1u    /* write full final node state (needed by dash_read_state) */
 #define DASH_TIER_FROM_32 2u  /* start at queue depth 32 (testing: exercises that kernel) */
-#define DASH_TIER_FROM_256 4u /* run every system at depth 256 directly */
-#define DASH_TIER_FROM_16 8u  /* start at queue depth 16; with no TIER flag the first depth
-                                 adapts to the previous run's overflow rate */
+#define DASH_TIER_FROM_256 4u /* run every system at depth 256 directly; with no TIER flag
+                                 the first depth adapts to the previous run's overflow rate */
 
 typedef struct dash_cfg {
     uint32_t num_procs;   /* NUM_PROCS (ref :6): 4 or 8 */
@@ -105,7 +104,7 @@ typedef struct dash_stats {
     uint64_t dropped;            /* messages dropped */
     uint64_t max_depth;          /* deepest queue after any delivery */
     double kernel_ms;            /* simulation kernel time (HIP events, engine stream) */
-    uint64_t tier_systems[DASH_NUM_TIERS]; /* systems simulated at queue depth 12, 16, 32, 256 */
+    uint64_t tier_systems[DASH_NUM_TIERS]; /* systems simulated at queue depth 16, 32, 256 */
 } dash_stats;
 
 /* Synthetic trace generator (counter-based, identical host spec in DESIGN.md §gen). */

@@ -130,10 +130,10 @@ def test_contention_and_small_address_space(dash, N):
 DEEP_SYSTEMS = [16, 67, 105, 199, 230, 236, 285, 309, 332]
 
 
-@pytest.mark.parametrize("flags", [0, 8, 2, 4])
+@pytest.mark.parametrize("flags", [0, 2, 4])
 def test_queue_depth_tiers(dash, flags):
     """Deep queues: systems that would fill a shallow LDS ring are handed to the
-    next depth (12 -> 16 -> 32 -> 256) and re-simulated from scratch; every
+    next depth (16 -> 32 -> 256) and re-simulated from scratch; every
     tier's kernel must give the oracle's result (queue capacity 256), and the
     hand-offs must be exactly the systems whose unbounded queues exceed each depth."""
     ids = DEEP_SYSTEMS + [0, 1, 2, 3, 4, 5, 6]
@@ -143,11 +143,11 @@ def test_queue_depth_tiers(dash, flags):
     depth = [run_system(packed[i], lens[i], num_procs=8, cache_size=4, ring_depth=256).max_depth
              for i in range(len(ids))]
     stats = check_batch(dash, packed, lens, 8, 4, flags=flags)
-    first = {0: 0, 8: 1, 2: 2, 4: 3}[flags]
-    tiers = [12, 16, 32, 256]
-    expect = [0] * 4
+    first = {0: 0, 2: 1, 4: 2}[flags]
+    tiers = [16, 32, 256]
+    expect = [0] * 3
     expect[first] = len(ids)
-    for k in range(first + 1, 4):
+    for k in range(first + 1, 3):
         expect[k] = sum(d > tiers[k - 1] for d in depth)
     assert stats["tier_systems"] == expect
     assert stats["max_depth"] > 16
@@ -157,8 +157,8 @@ def test_queue_depth_tiers(dash, flags):
 def test_adaptive_first_tier(dash):
     """Without a TIER flag, a run in which > 1/32 of the systems overflowed the
     first depth makes the next run start one depth deeper; results are unchanged."""
-    L, nsys = 1024, 64
-    with dash.Engine(nsys, num_procs=8, cache_size=4, max_instr=L) as eng:
+    L, nsys = 4096, 64
+    with dash.Engine(nsys, num_procs=8, cache_size=1, max_instr=L) as eng:
         eng.generate(0x5EED, L, kind=dash.GEN_CONTENTION)
         s1 = eng.run()
         d1 = eng.read_results()[0].copy()

@@ -244,8 +244,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
     uint64_t todo = h->cfg.num_systems;
     const uint32_t* list = nullptr;
     const uint32_t f = h->cfg.flags;
-    const int first = (f & DASH_TIER_FROM_256) ? 3 : (f & DASH_TIER_FROM_32) ? 2 : (f & DASH_TIER_FROM_16) ? 1
-                                                                                                   : h->auto_tier;
+    const int first = (f & DASH_TIER_FROM_256) ? 2 : (f & DASH_TIER_FROM_32) ? 1 : h->auto_tier;
     for (int tier = 0; tier < dash::NUM_TIERS; ++tier) h->tier_systems[tier] = 0;
     for (int tier = first; tier < dash::NUM_TIERS; ++tier) {
         const bool last = tier == dash::NUM_TIERS - 1;
@@ -268,7 +267,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
         todo = next;
         list = out;
     }
-    if (!(f & (DASH_TIER_FROM_16 | DASH_TIER_FROM_32 | DASH_TIER_FROM_256)) && first < dash::NUM_TIERS - 1 &&
+    if (!(f & (DASH_TIER_FROM_32 | DASH_TIER_FROM_256)) && first < dash::NUM_TIERS - 1 &&
         h->tier_systems[first + 1] * 32 > h->tier_systems[first])
         h->auto_tier = first + 1;
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));

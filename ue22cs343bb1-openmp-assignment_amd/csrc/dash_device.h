@@ -68,8 +68,8 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring
 
 // queue-depth tiers: each re-runs the systems that overflowed the previous one;
 // the last is the reference's MSG_BUFFER_SIZE (ref :9) and drops like it
-constexpr int NUM_TIERS = 4;
-constexpr uint32_t RING_TIERS[NUM_TIERS] = {12, 16, 32, 256};
+constexpr int NUM_TIERS = 3;
+constexpr uint32_t RING_TIERS[NUM_TIERS] = {16, 32, 256};
 constexpr uint32_t CHUNK_INSTR = 4;  // instructions per 8-B trace chunk
 hipError_t launch_gen(const GenArgs& g, hipStream_t s);
 

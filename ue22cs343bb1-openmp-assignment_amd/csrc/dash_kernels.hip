@@ -72,12 +72,10 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t WORDS = DUM + 64;
 };
 
-// ring index arithmetic for any depth R (x < 2R)
-template <uint32_t R>
-__device__ __forceinline__ uint32_t wrap(uint32_t x) {
-    if constexpr ((R & (R - 1)) == 0) return x & (R - 1);
-    else return x >= R ? x - R : x;
-}
+// wave-wide vote without HIP's int round trip (bool -> 0/1 -> compare)
+__device__ __forceinline__ uint64_t vote(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+// keeps a rarely taken branch a branch (no if-conversion onto the common path)
+#define COLD() asm volatile("" ::: "memory")
 
 template <int P, int CS, uint32_t RING>
 __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
@@ -116,6 +114,10 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     for (uint32_t i = 0; i < CS; ++i) lds16[L::CAC * 2 + i * 64 + sw] = 0xFFu;
     for (uint32_t w = lane; w < 13 * L::HSTRIDE; w += 64) lds[L::HST + w] = 0u;
     lds[L::MQ + 2 * lane] = 0u;
+    char* const ldsb = reinterpret_cast<char*>(lds);
+    constexpr uint32_t SLOT = 64 * 4;                 // bytes per ring slot (one word per lane)
+    constexpr uint32_t RMASK = RING * SLOT - 1;       // RING is a power of two
+    constexpr bool FINAL = RING == 256;               // the reference's capacity: exact drops
     uint32_t dsv = 0xAAAAAAAAu;  // 16 x U
     uint32_t cst = 0xFFFFFFFFu;  // CS x INVALID
 
@@ -137,11 +139,13 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     uint2 pend = make_uint2(0, 0);
     if (pend_idx < nch) pend = tr[pend_idx * 64];
 
-    // this node's incoming queue (messageBuffer, ref :81-87): count and tail of
-    // its LDS ring, owned by the node; senders learn them through MQ each round
-    uint32_t cnt = 0, tail = 0;
+    // this node's incoming queue (messageBuffer, ref :81-87): tail and count of
+    // its LDS ring in ring-slot bytes (x SLOT), owned by the node; senders learn
+    // them through MQ each round. Below the final depth the count is not clamped:
+    // exceeding RING is the overflow that hands the system to the next depth.
+    uint32_t cq = 0, tq = 0;
     uint32_t pc = 0, waiting = 0, last_val = 0;
-    uint32_t err = 0, maxd = 0, drops = 0;
+    uint32_t err = 0, maxd = 0, drops = 0;  // maxd in ring-slot bytes until the end
     uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
     const uint32_t cap = a.max_rounds;
 
@@ -150,20 +154,24 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         // A system is active while any of its nodes has a message or can issue;
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
         bool can_issue = (waiting == 0) & (pc < len);
-        bool active = (cnt != 0) | can_issue;
-        const uint64_t act = __ballot(active);
+        bool active = (cq != 0) | can_issue;
+        const uint64_t act = vote(active);
         if (act == 0) break;
         if (r == cap) {  // wave-uniform: every system still active has run `cap` rounds
+            COLD();
             if (((uint32_t)(act >> seg) & SEGMASK) != 0) {
                 err |= DASH_ERR_ROUNDCAP_D;
-                cnt = 0;
+                cq = 0;
                 len = pc;
                 waiting = 0;
                 can_issue = false;
                 active = false;
             }
         }
-        last_act = active ? r : last_act;
+        if (active) {
+            COLD();
+            last_act = r;
+        }
 
         // ---- wave-uniform housekeeping: trace window refill ----
         // Invariant at a refill point: pend_idx >= pc/CHUNK + 1 and the window holds
@@ -173,10 +181,10 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         if ((r & (CHUNK - 1)) == 0) {
             // a non-final tier stops a system soon after its first overflow: it will be
             // re-simulated from scratch at the next depth, its results here are void
-            if (a.final_tier == 0) {
-                const uint64_t ovf = __ballot((err & DASH_ERR_OVERFLOW_D) != 0);
+            if constexpr (!FINAL) {
+                const uint64_t ovf = vote(maxd > RING * SLOT);
                 if (ovf != 0 && ((uint32_t)(ovf >> seg) & SEGMASK) != 0) {
-                    cnt = 0;
+                    cq = 0;
                     len = pc;
                     waiting = 0;
                 }
@@ -189,12 +197,12 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         }
 
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
-        const bool has_msg = cnt != 0;
-        const uint32_t m = lds[L::RNG + wrap<RING>(tail + RING - cnt) * 64 + lane];
+        const bool has_msg = cq != 0;
+        const uint32_t m = *reinterpret_cast<const uint32_t*>(ldsb + L::RNG * 4 + ((tq - cq) & RMASK) + lane * 4);
         const uint32_t ins = lds16[L::WND * 2 + (pc % (WIN * CHUNK)) * 64 + sw];
         const bool do_issue = !has_msg & can_issue;
         pc += do_issue ? 1u : 0u;
-        cnt -= has_msg ? 1u : 0u;
+        cq -= has_msg ? SLOT : 0u;
         // message addresses are < 0x80 (a send to a node >= N is dropped), so bits
         // 14..8 give the address of a message and of an instruction alike
         const uint32_t mw = has_msg ? m : ins;
@@ -305,7 +313,8 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         waiting = ((iR & !hit) | (iW & !own_hit)) ? 1u : ((RRD | RWR | RID | FLUSH | FIA) ? 0u : waiting);
         last_val = do_issue ? ival : last_val;
         const bool oob = ev & !inN;  // ref UB: messageBuffers[15] -> drop + flag
-        if (__ballot(oob | ctz0) != 0) {  // rare: keep the counting off the common path
+        if (vote(oob | ctz0) != 0) {  // rare: keep the counting off the common path
+            COLD();
             err |= (oob ? DASH_ERR_OOB_D : 0u) | (ctz0 ? DASH_ERR_CTZ0_D : 0u);
             drops += (oob ? 1u : 0u) + (ctz0 ? 1u : 0u);
         }
@@ -324,48 +333,59 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         // ref :364-379): a sender's slot is the receiver's tail plus the number of
         // bits below its own, and the receiver's capacity check (ref :754-761)
         // compares the receiver's count plus that rank with the ring depth.
-        lds[L::MQ + 2 * lane + 1] = tail | (cnt << 16);
+        lds[L::MQ + 2 * lane + 1] = tq | (cq << 8);  // tail byte offset | count << 16
         const uint32_t bitP = 2u << (4 * t), bitB = 4u << (4 * t), bitI = 1u << (4 * t);
         if (vP)
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (vB)
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const bool any_inv = __ballot(inv != 0) != 0;
+        const bool any_inv = vote(inv != 0) != 0;
         if (any_inv) {
+            COLD();
             uint32_t im = inv;
             do {
                 if (im != 0)
                     __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + ((uint32_t)__builtin_ctz(im) & 7u))], bitI,
                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 im &= im - 1u;
-            } while (__ballot(im != 0) != 0);
+            } while (vote(im != 0) != 0);
         }
         auto place = [&](bool v, uint32_t d, uint32_t bit, uint32_t w) {
             const uint2 q = *reinterpret_cast<const uint2*>(&lds[L::MQ + 2 * (seg + d)]);
             const uint32_t rank = (uint32_t)__builtin_popcount(q.x & (bit - 1u));
-            const bool ok = v & (((q.y >> 16) + rank) < RING);
-            const uint32_t slot = wrap<RING>((q.y & 0xFFFFu) + rank);  // used only when ok
-            lds[ok ? (L::RNG + slot * 64 + seg + d) : (L::DUM + lane)] = w;
-            const bool lost = v & !ok;
-            err |= lost ? DASH_ERR_OVERFLOW_D : 0u;
-            drops += lost ? 1u : 0u;
+            // slot byte offset = receiver tail + rank slots (the count bits above
+            // bit 15 fall off the mask)
+            const uint32_t off = ((q.y + (rank << 8)) & RMASK) | ((seg + d) * 4);
+            if constexpr (FINAL) {
+                const bool ok = v & ((q.y >> 16) + rank < RING);
+                *reinterpret_cast<uint32_t*>(ldsb + (ok ? L::RNG * 4 + off : L::DUM * 4 + lane * 4)) = w;
+                if (vote(v & !ok) != 0) {
+                    COLD();
+                    err |= (v & !ok) ? DASH_ERR_OVERFLOW_D : 0u;
+                    drops += (v & !ok) ? 1u : 0u;
+                }
+            } else {
+                *reinterpret_cast<uint32_t*>(ldsb + (v ? L::RNG * 4 + off : L::DUM * 4 + lane * 4)) = w;
+            }
         };
         place(vP, dP, bitP, wP);
         place(vB, msr, bitB, wA);
         if (any_inv) {
+            COLD();
             const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
             uint32_t im = inv;
             do {
                 place(im != 0, (uint32_t)__builtin_ctz(im | 0x100u) & 7u, bitI, winv);
                 im &= im - 1u;
-            } while (__ballot(im != 0) != 0);
+            } while (vote(im != 0) != 0);
         }
         const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQ + 2 * lane], 0u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t n = min((uint32_t)__builtin_popcount(arrived), RING - cnt);
-        tail = wrap<RING>(tail + n);
-        cnt += n;
-        maxd = max(maxd, cnt);
+        uint32_t n = (uint32_t)__builtin_popcount(arrived) << 8;
+        if constexpr (FINAL) n = min(n, RING * SLOT - cq);  // sendMessage's drop (ref :754-761)
+        tq = (tq + n) & RMASK;
+        cq += n;
+        maxd = max(maxd, cq);
     }
 
     // ---- results ----
@@ -378,7 +398,10 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         rounds = max(rounds, (uint32_t)__shfl_xor(rounds, n, P));
     }
     // a non-final tier hands overflowed systems to the next tier: no outputs, no statistics
-    const bool handoff = a.final_tier == 0 && (serr & DASH_ERR_OVERFLOW_D) != 0;
+    bool ovf_sys = !FINAL && maxd > RING * SLOT;
+#pragma unroll
+    for (uint32_t n = 1; n < P; n <<= 1) ovf_sys |= __shfl_xor((int)ovf_sys, n, P) != 0;
+    const bool handoff = ovf_sys;
     const bool report = live && !handoff;
 
     uint32_t hcnt[13];  // this system's per-type counts (read by its node-0 lane)
@@ -402,6 +425,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         a.errors[sys] = serr;
     }
     if (live && t == 0 && handoff) a.ovf_list[atomicAdd(a.ovf_count, 1u)] = (uint32_t)sys;
+    maxd >>= 8;  // ring-slot bytes -> messages
     if (a.state && report) {
         uint32_t* st = a.state + (sys * N + t) * (16 + CS);
         for (uint32_t b = 0; b < 16; ++b)
@@ -511,7 +535,6 @@ static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t 
 template <int P, int CS>
 static hipError_t launch_sim_pc(const SimArgs& a, uint32_t ring, uint64_t groups, hipStream_t s) {
     switch (ring) {
-    case 12: return launch_sim_pcr<P, CS, 12>(a, groups, s);
     case 16: return launch_sim_pcr<P, CS, 16>(a, groups, s);
     case 32: return launch_sim_pcr<P, CS, 32>(a, groups, s);
     case 256: return launch_sim_pcr<P, CS, 256>(a, groups, s);

@@ -39,8 +39,8 @@ TXN_NAMES = ("READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID"
 OK, EINVAL, EIO, EPARSE, EADDR, EDEVICE, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5, -6, -7
 ERR_OVERFLOW, ERR_OOB, ERR_CTZ0, ERR_DEADLOCK, ERR_ROUNDCAP = 1, 2, 4, 8, 16
 KEEP_STATE = 1
-TIER_FROM_32, TIER_FROM_256, TIER_FROM_16 = 2, 4, 8
-NUM_TIERS = 4
+TIER_FROM_32, TIER_FROM_256 = 2, 4
+NUM_TIERS = 3
 GEN_UNIFORM, GEN_CONTENTION, GEN_LOCALITY = 0, 1, 2
 
 # every symbol include/dash.h declares

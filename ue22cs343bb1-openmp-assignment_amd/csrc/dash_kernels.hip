@@ -155,10 +155,9 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
         bool can_issue = (waiting == 0) & (pc < len);
         bool active = (cq != 0) | can_issue;
-        const uint64_t act = vote(active);
-        if (act == 0) break;
         if (r == cap) {  // wave-uniform: every system still active has run `cap` rounds
             COLD();
+            const uint64_t act = vote(active);
             if (((uint32_t)(act >> seg) & SEGMASK) != 0) {
                 err |= DASH_ERR_ROUNDCAP_D;
                 cq = 0;
@@ -179,6 +178,9 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         // the chunks read until the next refill point (pc/CHUNK, pc/CHUNK + 1) are
         // always resident; the pending chunk's load has CHUNK rounds to land.
         if ((r & (CHUNK - 1)) == 0) {
+            // quiescence is absorbing, so testing it every CHUNK rounds only adds
+            // idle rounds (no state changes, not counted in `rounds`)
+            if (vote(active) == 0) break;
             // a non-final tier stops a system soon after its first overflow: it will be
             // re-simulated from scratch at the next depth, its results here are void
             if constexpr (!FINAL) {
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         const uint32_t ins = lds16[L::WND * 2 + (pc % (WIN * CHUNK)) * 64 + sw];
         const bool do_issue = !has_msg & can_issue;
         pc += do_issue ? 1u : 0u;
-        cq -= has_msg ? SLOT : 0u;
+        cq = __builtin_elementwise_sub_sat(cq, SLOT);  // pop (cq is a multiple of SLOT)
         // message addresses are < 0x80 (a send to a node >= N is dropped), so bits
         // 14..8 give the address of a message and of an instruction alike
         const uint32_t mw = has_msg ? m : ins;
@@ -210,8 +212,10 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         const uint32_t idx = b & (CS - 1);
-        const uint32_t e16 = lds16[L::ENT * 2 + b * 64 + sw];
-        const uint32_t c16 = lds16[L::CAC * 2 + idx * 64 + sw];
+        uint16_t* const ent = lds16 + L::ENT * 2 + b * 64 + sw;
+        uint16_t* const cac = lds16 + L::CAC * 2 + idx * 64 + sw;
+        const uint32_t e16 = *ent;
+        const uint32_t c16 = *cac;
         const uint32_t mty = m & 15u;
         if (has_msg)  // messages handled per transactionType, per system
             __hip_atomic_fetch_add(&lds[L::HST + mty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
@@ -308,19 +312,18 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         const uint32_t wP = vA ? wA : wE;
         // second copy of a flush: WRITEBACK_INV always (:498), WRITEBACK_INT if sr != home (:281)
         const bool vB = WBINV | (WBINT & (H != msr));
-        const uint32_t inv = RID ? (mval & rcv_mask) : 0u;  // REPLY_ID fan-out (:364-373)
 
         waiting = ((iR & !hit) | (iW & !own_hit)) ? 1u : ((RRD | RWR | RID | FLUSH | FIA) ? 0u : waiting);
         last_val = do_issue ? ival : last_val;
         const bool oob = ev & !inN;  // ref UB: messageBuffers[15] -> drop + flag
-        if (vote(oob | ctz0) != 0) {  // rare: keep the counting off the common path
+        if (oob | ctz0) {  // rare: keep the counting off the common path
             COLD();
             err |= (oob ? DASH_ERR_OOB_D : 0u) | (ctz0 ? DASH_ERR_CTZ0_D : 0u);
             drops += (oob ? 1u : 0u) + (ctz0 ? 1u : 0u);
         }
 
-        lds16[L::ENT * 2 + b * 64 + sw] = (uint16_t)(nmem | (nbv << 8));
-        lds16[L::CAC * 2 + idx * 64 + sw] = (uint16_t)(fill ? (addr | (fval << 8)) : c16);
+        *ent = (uint16_t)(nmem | (nbv << 8));
+        *cac = (uint16_t)(fill ? (addr | (fval << 8)) : c16);
         dsv = (dsv & ~(3u << (2 * b))) | (nds << (2 * b));
         cst = (cst & ~(3u << (2 * idx))) | (nst << (2 * idx));
 
@@ -339,16 +342,11 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (vB)
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const bool any_inv = vote(inv != 0) != 0;
-        if (any_inv) {
+        if (RID) {  // REPLY_ID's INV fan-out (ref :364-373): ascending receivers
             COLD();
-            uint32_t im = inv;
-            do {
-                if (im != 0)
-                    __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + ((uint32_t)__builtin_ctz(im) & 7u))], bitI,
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                im &= im - 1u;
-            } while (vote(im != 0) != 0);
+            for (uint32_t im = mval & rcv_mask; im != 0; im &= im - 1u)
+                __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + (uint32_t)__builtin_ctz(im))], bitI,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         auto place = [&](bool v, uint32_t d, uint32_t bit, uint32_t w) {
             const uint2 q = *reinterpret_cast<const uint2*>(&lds[L::MQ + 2 * (seg + d)]);
@@ -370,14 +368,11 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         };
         place(vP, dP, bitP, wP);
         place(vB, msr, bitB, wA);
-        if (any_inv) {
+        if (RID) {
             COLD();
             const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
-            uint32_t im = inv;
-            do {
-                place(im != 0, (uint32_t)__builtin_ctz(im | 0x100u) & 7u, bitI, winv);
-                im &= im - 1u;
-            } while (vote(im != 0) != 0);
+            for (uint32_t im = mval & rcv_mask; im != 0; im &= im - 1u)
+                place(true, (uint32_t)__builtin_ctz(im), bitI, winv);
         }
         const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQ + 2 * lane], 0u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -24,6 +24,7 @@ import time
 ROOT = pathlib.Path(__file__).resolve().parent
 PEAK_HBM = 8.0e12  # B/s, MI355X_MICROARCH.md chip table
 BYTES_PER_INSTR = 2  # packed trace record read once
+VALU_PEAK = 256 * 2.4e9  # wave-instr/s: 256 CUs x 1 VALU issue per cycle x 2.4 GHz
 
 
 def load_dash():
@@ -75,12 +76,13 @@ def reduce_totals(elapsed, counters, device, world):
     return float(t.item()), [int(x) for x in c.tolist()]
 
 
-def read_traffic(kind):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
-    f = ROOT / "profiles" / f"traffic_{kind}.json"
+def read_profile(kind):
+    """Per-launch counters of the first-tier sim_kernel from the committed rocprofv3
+    PMC summary for this workload (tools/pmc_summary.py), or None."""
+    f = ROOT / "profiles" / f"pmc_{kind}.json"
     if f.exists():
         try:
-            return json.loads(f.read_text()).get("hbm_bytes_per_launch")
+            return json.loads(f.read_text())
         except Exception:
             return None
     return None
@@ -152,6 +154,7 @@ def main():
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     achieved = M * 8 * args.len * BYTES_PER_INSTR / avg_kernel_s
 
+    prof = read_profile(args.kind) if (M == 1 << 20 and args.len == 4096 and args.cache_size == 4) else None
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -176,10 +179,18 @@ def main():
                        "parallelism": f"systems sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM,
-                         "traffic": read_traffic(args.kind)},
+                         "traffic": prof.get("hbm_bytes_per_launch") if prof else None},
+            # the bound that actually binds this integer state machine: VALU issue,
+            # one wave-instruction per cycle per CU
+            "valu_issue": ({"achieved": prof["valu_per_launch"] / avg_kernel_s,
+                            "peak": VALU_PEAK, "unit": "wave-instr/s",
+                            "frac": prof["valu_per_launch"] / avg_kernel_s / VALU_PEAK,
+                            "valu_per_round": prof.get("valu_per_wave_round"),
+                            "source": prof.get("source")} if prof else None),
             "cpu_baseline": cpu,
             "kernel_ms_avg": avg_kernel_s * 1e3,
             "tier_systems": stats["tier_systems"],
+            "wave_rounds": stats["wave_rounds"],
             "totals": {"hist": totals[:13], "instructions_per_step": totals[13],
                        "rounds_total": totals[14], "err_systems": totals[15], "dropped": totals[16]},
         }

@@ -105,6 +105,7 @@ typedef struct dash_stats {
     uint64_t max_depth;          /* deepest queue after any delivery */
     double kernel_ms;            /* simulation kernel time (HIP events, engine stream) */
     uint64_t tier_systems[DASH_NUM_TIERS]; /* systems simulated at queue depth 16, 32, 256 */
+    uint64_t wave_rounds;        /* lockstep-loop trips summed over wavefronts (all tiers) */
 } dash_stats;
 
 /* Synthetic trace generator (counter-based, identical host spec in DESIGN.md §gen). */

@@ -290,6 +290,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
         stats->max_depth = s[dash::STAT_MAXDEPTH];
         stats->kernel_ms = ms;
         for (int k = 0; k < dash::NUM_TIERS; k++) stats->tier_systems[k] = h->tier_systems[k];
+        stats->wave_rounds = s[dash::STAT_WAVE_ROUNDS];
     }
     return DASH_OK;
 }

@@ -23,6 +23,7 @@ enum : uint32_t {
     STAT_ERRBITS = 18,
     STAT_DROPS = 19,
     STAT_MAXDEPTH = 20,
+    STAT_WAVE_ROUNDS = 21,  // loop trips summed over waves (the kernel's unit of work)
     STAT_WORDS = 32
 };
 

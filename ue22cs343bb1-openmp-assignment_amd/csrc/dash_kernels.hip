@@ -149,7 +149,8 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
     const uint32_t cap = a.max_rounds;
 
-    for (uint32_t r = 0;; ++r) {
+    uint32_t r = 0;
+    for (;; ++r) {
         // ---- quiescence / round cap, on start-of-round state ----
         // A system is active while any of its nodes has a message or can issue;
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
@@ -467,6 +468,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         if (ebits) atomicOr(&S[STAT_ERRBITS], (unsigned long long)ebits);
         if (s_drops) atomicAdd(&S[STAT_DROPS], (unsigned long long)s_drops);
         atomicMax(&S[STAT_MAXDEPTH], (unsigned long long)m_depth);
+        atomicAdd(&S[STAT_WAVE_ROUNDS], (unsigned long long)r);
     }
 }
 

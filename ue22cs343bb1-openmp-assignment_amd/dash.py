@@ -76,7 +76,7 @@ class Stats(ctypes.Structure):
                 ("systems", ctypes.c_uint64), ("err_systems", ctypes.c_uint64),
                 ("err_bits", ctypes.c_uint64), ("dropped", ctypes.c_uint64),
                 ("max_depth", ctypes.c_uint64), ("kernel_ms", ctypes.c_double),
-                ("tier_systems", ctypes.c_uint64 * NUM_TIERS)]
+                ("tier_systems", ctypes.c_uint64 * NUM_TIERS), ("wave_rounds", ctypes.c_uint64)]
 
     def as_dict(self):
         return {"hist": [int(x) for x in self.hist], "instructions": int(self.instructions),
@@ -84,7 +84,8 @@ class Stats(ctypes.Structure):
                 "systems": int(self.systems), "err_systems": int(self.err_systems),
                 "err_bits": int(self.err_bits), "dropped": int(self.dropped),
                 "max_depth": int(self.max_depth), "kernel_ms": float(self.kernel_ms),
-                "tier_systems": [int(x) for x in self.tier_systems]}
+                "tier_systems": [int(x) for x in self.tier_systems],
+                "wave_rounds": int(self.wave_rounds)}
 
 
 class Gen(ctypes.Structure):

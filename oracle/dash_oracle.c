@@ -626,3 +626,332 @@ int orc_dump_node(const orc_node_state *s, int id, int cache_size, char *buf, in
 #undef P
     return n;
 }
+
+/* ==== legality checker: the race-free micro-step model ====
+ *
+ * A reference thread's observable behaviour is a sequence of operations on the
+ * shared queues (:102): pops from its own queue (:167-177) and appends to other
+ * queues (sendMessage :741-765); everything else touches thread-private state
+ * (private(node), :149). The micro-step model has one step kind per such
+ * operation, with each thread's sends buffered in an outbox (FIFO) between the
+ * handler that produced them and the append -- any gap is a legal delay of the
+ * sending thread:
+ *   POP(t)    pop t's queue head and run the handler (local effects, sends -> outbox)
+ *   ISSUE(t)  t's queue is empty, t is not waiting, instructions remain (:624-647):
+ *             issue one instruction (local effects, sends -> outbox)
+ *   SEND(t)   append the head of t's outbox to its receiver's queue
+ * Every total order of enabled steps is a legal execution of the reference
+ * with race-free queues (App. B 12: the unlocked count-- race is the
+ * reference's bug, not part of its semantics). Terminal: no step enabled.
+ *
+ * Exhaustive search uses the persistent set {POP(t)} for the lowest t with a
+ * non-empty queue: a pop commutes with every other thread's steps (appends go to
+ * the tail of a non-empty queue) and with t's own SEND (outbox FIFO), and no
+ * other step of t is enabled while t's queue is non-empty, so terminal states
+ * are preserved. */
+
+#define XQ 40 /* explorer per-node queue / outbox capacity */
+
+typedef struct {
+    oline cache[ORC_MAX_CACHE];
+    uint8_t memory[ORC_MEM_SIZE], bitVector[ORC_MEM_SIZE], dirState[ORC_MEM_SIZE];
+    uint16_t idx;
+    uint8_t waiting, instr_value, qn, on, _pad[2];
+    omsg q[XQ];        /* incoming queue, head first */
+    omsg o[XQ];        /* outbox, head first */
+    uint8_t oto[XQ];   /* outbox receivers */
+} xnode;
+
+typedef struct {
+    xnode n[ORC_MAX_PROCS];
+    uint32_t errors;
+    uint32_t _pad;
+} xsys;
+
+typedef struct {
+    int N, CS;
+    const uint16_t *trace[ORC_MAX_PROCS];
+    uint32_t count[ORC_MAX_PROCS];
+    osys *scratch; /* the oracle's handlers run on a scratch node */
+    orc_result scratch_res;
+} xctx;
+
+static void x_init(xctx *c, xsys *s) {
+    memset(s, 0, sizeof *s);
+    for (int t = 0; t < c->N; t++) {
+        onode tmp;
+        init_node(&tmp, t, c->CS);
+        xnode *x = &s->n[t];
+        memcpy(x->cache, tmp.cache, sizeof x->cache);
+        memcpy(x->memory, tmp.memory, sizeof x->memory);
+        memcpy(x->bitVector, tmp.bitVector, sizeof x->bitVector);
+        memcpy(x->dirState, tmp.dirState, sizeof x->dirState);
+    }
+}
+
+/* run one POP (msg != NULL) or ISSUE step of node t through the oracle's handlers */
+static void x_step(xctx *c, xsys *s, int t, const omsg *msg) {
+    xnode *x = &s->n[t];
+    onode *nd = &c->scratch->node[t];
+    memcpy(nd->cache, x->cache, sizeof x->cache);
+    memcpy(nd->memory, x->memory, sizeof x->memory);
+    memcpy(nd->bitVector, x->bitVector, sizeof x->bitVector);
+    memcpy(nd->dirState, x->dirState, sizeof x->dirState);
+    nd->trace = c->trace[t];
+    nd->count = c->count[t];
+    nd->idx = x->idx;
+    nd->waiting = x->waiting;
+    nd->instr_value = x->instr_value;
+    nd->nout = 0;
+    c->scratch->res = &c->scratch_res;
+    c->scratch_res.errors = 0;
+    if (msg)
+        handle_message(c->scratch, t, *msg);
+    else
+        issue_instruction(c->scratch, t);
+    s->errors |= c->scratch_res.errors;
+    memcpy(x->cache, nd->cache, sizeof x->cache);
+    memcpy(x->memory, nd->memory, sizeof x->memory);
+    memcpy(x->bitVector, nd->bitVector, sizeof x->bitVector);
+    memcpy(x->dirState, nd->dirState, sizeof x->dirState);
+    x->idx = (uint16_t)nd->idx;
+    x->waiting = (uint8_t)nd->waiting;
+    x->instr_value = nd->instr_value;
+    for (int k = 0; k < nd->nout; k++) {
+        if (x->on >= XQ) { s->errors |= ORC_ERR_OVERFLOW; continue; }
+        x->o[x->on] = nd->out[k];
+        x->oto[x->on] = (uint8_t)nd->out_to[k];
+        x->on++;
+    }
+}
+
+static void x_pop(xctx *c, xsys *s, int t) {
+    xnode *x = &s->n[t];
+    omsg m = x->q[0];
+    memmove(&x->q[0], &x->q[1], sizeof(omsg) * (size_t)(x->qn - 1));
+    x->qn--;
+    memset(&x->q[x->qn], 0, sizeof(omsg));
+    x_step(c, s, t, &m);
+}
+
+static void x_send(xctx *c, xsys *s, int t) {
+    xnode *x = &s->n[t];
+    omsg m = x->o[0];
+    int rcv = x->oto[0];
+    memmove(&x->o[0], &x->o[1], sizeof(omsg) * (size_t)(x->on - 1));
+    memmove(&x->oto[0], &x->oto[1], (size_t)(x->on - 1));
+    x->on--;
+    memset(&x->o[x->on], 0, sizeof(omsg));
+    x->oto[x->on] = 0;
+    if (rcv < 0 || rcv >= c->N) { s->errors |= ORC_ERR_OOB; return; }
+    xnode *d = &s->n[rcv];
+    if (d->qn >= XQ) { s->errors |= ORC_ERR_OVERFLOW; return; }
+    d->q[d->qn++] = m;
+}
+
+static int x_can_issue(const xctx *c, const xsys *s, int t) {
+    const xnode *x = &s->n[t];
+    return x->qn == 0 && !x->waiting && x->idx < c->count[t];
+}
+
+static uint64_t x_hash(const xsys *s) {
+    const uint64_t *w = (const uint64_t *)s;
+    uint64_t h = 0x243F6A8885A308D3ULL;
+    for (size_t i = 0; i < sizeof(xsys) / 8; i++) h = fmix64(h ^ w[i]) + (uint64_t)i;
+    return h;
+}
+
+static void x_outcome(const xctx *c, const xsys *s, orc_outcome *o) {
+    memset(o, 0, sizeof *o);
+    uint64_t d = 0x9E3779B97F4A7C15ULL;
+    for (int t = 0; t < c->N; t++) {
+        const xnode *x = &s->n[t];
+        orc_node_state *st = &o->node[t];
+        memcpy(st->memory, x->memory, ORC_MEM_SIZE);
+        memcpy(st->dir_bitvector, x->bitVector, ORC_MEM_SIZE);
+        memcpy(st->dir_state, x->dirState, ORC_MEM_SIZE);
+        for (int i = 0; i < c->CS; i++) {
+            st->cache_addr[i] = x->cache[i].address;
+            st->cache_value[i] = x->cache[i].value;
+            st->cache_state[i] = x->cache[i].state;
+        }
+        if (x->waiting) o->errors |= ORC_ERR_DEADLOCK;
+        d = fmix64(d ^ orc_digest_node(st, t, c->CS));
+    }
+    o->errors |= s->errors;
+    o->digest = d;
+}
+
+static int x_setup(xctx *c, const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens) {
+    memset(c, 0, sizeof *c);
+    c->N = cfg->num_procs;
+    c->CS = cfg->cache_size;
+    if (c->N < 1 || c->N > ORC_MAX_PROCS || c->CS < 1 || c->CS > ORC_MAX_CACHE || (c->CS & (c->CS - 1))) return -1;
+    for (int t = 0; t < c->N; t++) {
+        c->trace[t] = trace + (uint64_t)t * stride;
+        c->count[t] = lens[t];
+        if (lens[t] > 0xFFFF) return -1;
+        for (uint32_t i = 0; i < lens[t]; i++)
+            if (((c->trace[t][i] >> 12) & 0x7) >= (unsigned)c->N) return -1;
+    }
+    c->scratch = (osys *)calloc(1, sizeof(osys));
+    if (!c->scratch) return -1;
+    c->scratch->N = c->N;
+    c->scratch->CS = c->CS;
+    c->scratch->ring = MAX_RING;
+    return 0;
+}
+
+int orc_replay_lockstep(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                        orc_outcome *out, uint64_t *steps) {
+    xctx c;
+    if (x_setup(&c, cfg, trace, stride, lens)) return -1;
+    xsys *s = (xsys *)malloc(sizeof(xsys));
+    x_init(&c, s);
+    uint64_t n = 0;
+    int rc = 0;
+    for (;;) {
+        /* a lockstep round as micro-steps: every node's POP or ISSUE on start-of-round
+           queues (no SEND has run yet), then every outbox drained in sender order */
+        int any = 0;
+        int popq[ORC_MAX_PROCS];
+        for (int t = 0; t < c.N; t++) popq[t] = s->n[t].qn > 0;
+        for (int t = 0; t < c.N; t++) {
+            if (popq[t]) {
+                if (s->n[t].qn == 0) { rc = -2; break; } /* not enabled: cannot happen */
+                x_pop(&c, s, t);
+                any = 1;
+                n++;
+            } else if (x_can_issue(&c, s, t)) {
+                x_step(&c, s, t, NULL);
+                any = 1;
+                n++;
+            }
+        }
+        for (int t = 0; t < c.N; t++)
+            while (s->n[t].on > 0) { x_send(&c, s, t); n++; }
+        if (!any || rc) break;
+    }
+    x_outcome(&c, s, out);
+    if (steps) *steps = n;
+    free(s);
+    free(c.scratch);
+    return rc;
+}
+
+static uint64_t x_rng(uint64_t *st) {
+    *st += 0x9E3779B97F4A7C15ULL;
+    return fmix64(*st);
+}
+
+int orc_random_schedule(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                        uint64_t seed, orc_outcome *out) {
+    xctx c;
+    if (x_setup(&c, cfg, trace, stride, lens)) return -1;
+    xsys *s = (xsys *)malloc(sizeof(xsys));
+    x_init(&c, s);
+    uint64_t st = seed;
+    for (;;) {
+        int kinds[3 * ORC_MAX_PROCS], who[3 * ORC_MAX_PROCS], ne = 0;
+        for (int t = 0; t < c.N; t++) {
+            if (s->n[t].qn > 0) { kinds[ne] = 0; who[ne++] = t; }
+            if (x_can_issue(&c, s, t)) { kinds[ne] = 1; who[ne++] = t; }
+            if (s->n[t].on > 0) { kinds[ne] = 2; who[ne++] = t; }
+        }
+        if (ne == 0) break;
+        int k = (int)(x_rng(&st) % (uint64_t)ne);
+        if (kinds[k] == 0) x_pop(&c, s, who[k]);
+        else if (kinds[k] == 1) x_step(&c, s, who[k], NULL);
+        else x_send(&c, s, who[k]);
+    }
+    x_outcome(&c, s, out);
+    free(s);
+    free(c.scratch);
+    return 0;
+}
+
+typedef struct {
+    uint64_t *keys;
+    uint64_t cap, n;
+} xset;
+
+static int xset_insert(xset *v, uint64_t h) { /* 1 if newly inserted */
+    if (h == 0) h = 1;
+    uint64_t i = h & (v->cap - 1);
+    while (v->keys[i]) {
+        if (v->keys[i] == h) return 0;
+        i = (i + 1) & (v->cap - 1);
+    }
+    v->keys[i] = h;
+    v->n++;
+    return 1;
+}
+
+int orc_explore(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                uint64_t max_states, orc_outcome *outs, int max_outs, int *n_outs, uint64_t *states,
+                int *complete) {
+    xctx c;
+    if (x_setup(&c, cfg, trace, stride, lens)) return -1;
+    xset vis;
+    vis.cap = 1;
+    while (vis.cap < 2 * max_states + 2) vis.cap <<= 1;
+    vis.keys = (uint64_t *)calloc(vis.cap, sizeof(uint64_t));
+    vis.n = 0;
+    size_t scap = 1024, sn = 0;
+    xsys *stack = (xsys *)malloc(sizeof(xsys) * scap);
+    if (!vis.keys || !stack) { free(vis.keys); free(stack); free(c.scratch); return -1; }
+    int nout = 0, full = 1;
+    x_init(&c, &stack[sn++]);
+    xset_insert(&vis, x_hash(&stack[0]));
+    xsys cur, nxt;
+    while (sn > 0) {
+        cur = stack[--sn];
+        int succ_kind[3 * ORC_MAX_PROCS], succ_who[3 * ORC_MAX_PROCS], ns = 0;
+        int popper = -1;
+        for (int t = 0; t < c.N; t++)
+            if (cur.n[t].qn > 0) { popper = t; break; }
+        if (popper >= 0) { /* persistent set {POP(popper)} */
+            succ_kind[ns] = 0;
+            succ_who[ns++] = popper;
+        } else {
+            for (int t = 0; t < c.N; t++) {
+                if (x_can_issue(&c, &cur, t)) { succ_kind[ns] = 1; succ_who[ns++] = t; }
+                if (cur.n[t].on > 0) { succ_kind[ns] = 2; succ_who[ns++] = t; }
+            }
+        }
+        if (ns == 0) { /* terminal: record the outcome if new */
+            orc_outcome o;
+            x_outcome(&c, &cur, &o);
+            int seen = 0;
+            for (int k = 0; k < nout && k < max_outs; k++)
+                if (outs[k].digest == o.digest) seen = 1;
+            if (!seen) {
+                if (nout < max_outs) outs[nout] = o;
+                nout++;
+            }
+            continue;
+        }
+        for (int k = 0; k < ns; k++) {
+            nxt = cur;
+            if (succ_kind[k] == 0) x_pop(&c, &nxt, succ_who[k]);
+            else if (succ_kind[k] == 1) x_step(&c, &nxt, succ_who[k], NULL);
+            else x_send(&c, &nxt, succ_who[k]);
+            if (vis.n >= max_states) { full = 0; continue; }
+            if (!xset_insert(&vis, x_hash(&nxt))) continue;
+            if (sn == scap) {
+                scap *= 2;
+                xsys *ns2 = (xsys *)realloc(stack, sizeof(xsys) * scap);
+                if (!ns2) { full = 0; break; }
+                stack = ns2;
+            }
+            stack[sn++] = nxt;
+        }
+    }
+    if (n_outs) *n_outs = nout;
+    if (states) *states = vis.n;
+    if (complete) *complete = full;
+    free(vis.keys);
+    free(stack);
+    free(c.scratch);
+    return 0;
+}

@@ -79,6 +79,12 @@ def lib():
         L.orc_dump_node.argtypes = [ctypes.POINTER(OrcNodeState), ctypes.c_int, ctypes.c_int,
                                     ctypes.c_char_p, ctypes.c_int]
         L.orc_dump_node.restype = ctypes.c_int
+        V, U64 = ctypes.c_void_p, ctypes.c_uint64
+        L.orc_replay_lockstep.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, V]
+        L.orc_random_schedule.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, U64, V]
+        L.orc_explore.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, U64, V, ctypes.c_int, V, V, V]
+        for f in (L.orc_replay_lockstep, L.orc_random_schedule, L.orc_explore):
+            f.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -138,6 +144,56 @@ def run_system(trace, lens, num_procs=4, cache_size=4, ring_depth=256, max_round
     if rc != 0:
         raise ValueError("oracle rejected the configuration or trace")
     return (res, buf.value.decode()) if log else res
+
+
+class OrcOutcome(ctypes.Structure):
+    _fields_ = [("node", OrcNodeState * MAX_PROCS), ("digest", ctypes.c_uint64),
+                ("errors", ctypes.c_uint32), ("_pad", ctypes.c_uint32)]
+
+
+def _tr(trace, lens):
+    return (np.ascontiguousarray(trace, dtype=np.uint16), np.ascontiguousarray(lens, dtype=np.uint32))
+
+
+def replay_lockstep(trace, lens, num_procs=4, cache_size=4):
+    """The lockstep schedule as race-free micro-steps (legality checker)."""
+    trace, lens = _tr(trace, lens)
+    cfg = OrcCfg(num_procs, cache_size, 256, 0)
+    out = OrcOutcome()
+    steps = ctypes.c_uint64()
+    rc = lib().orc_replay_lockstep(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1], lens.ctypes.data,
+                                   ctypes.addressof(out), ctypes.addressof(steps))
+    if rc != 0:
+        raise ValueError(f"lockstep replay failed ({rc})")
+    return out, int(steps.value)
+
+
+def random_schedule(trace, lens, seed, num_procs=4, cache_size=4):
+    """Final state of one uniformly random legal micro-step schedule."""
+    trace, lens = _tr(trace, lens)
+    cfg = OrcCfg(num_procs, cache_size, 256, 0)
+    out = OrcOutcome()
+    if lib().orc_random_schedule(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1], lens.ctypes.data,
+                                 seed, ctypes.addressof(out)) != 0:
+        raise ValueError("random schedule failed")
+    return out
+
+
+def explore(trace, lens, num_procs=4, cache_size=4, max_states=1_000_000, max_outs=4096):
+    """Exhaustive search of the race-free micro-step model (pop-first persistent
+    sets). Returns (distinct outcomes, states visited, complete)."""
+    trace, lens = _tr(trace, lens)
+    cfg = OrcCfg(num_procs, cache_size, 256, 0)
+    outs = (OrcOutcome * max_outs)()
+    n = ctypes.c_int()
+    states = ctypes.c_uint64()
+    full = ctypes.c_int()
+    rc = lib().orc_explore(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1], lens.ctypes.data,
+                           max_states, ctypes.addressof(outs), max_outs, ctypes.addressof(n),
+                           ctypes.addressof(states), ctypes.addressof(full))
+    if rc != 0:
+        raise ValueError("explore failed")
+    return [outs[k] for k in range(min(n.value, max_outs))], int(states.value), bool(full.value)
 
 
 def dump_node(res, node, cache_size=4) -> str:

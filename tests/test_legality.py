@@ -1,0 +1,150 @@
+"""Legality of the lockstep schedule, CPU only.
+
+The oracle's race-free micro-step model (oracle/dash_oracle.c, legality
+checker) executes the reference's per-thread operations -- POP + handler,
+ISSUE, SEND (the append of one outbox message) -- in any order; every order is
+a legal execution of assignment.c with race-free queues. These tests check:
+  * the lockstep schedule replayed as micro-steps reaches the engine's final
+    state (it is one legal order: every node's POP/ISSUE on start-of-round
+    queues, then all SENDs in ascending sender order);
+  * exhaustive enumeration: `sample` has exactly two legal outcomes, the
+    reference's expected dump among them; test_1/test_2 split into independent
+    single-node components and have exactly one outcome, the expected one;
+  * uniformly random legal schedules of the racy tests land on the accepted
+    `run_*` outputs (run_1 and run_2 of test_3 and test_4 are legal outcomes).
+"""
+import collections
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+
+TESTS = ["sample", "test_1", "test_2", "test_3", "test_4"]
+
+
+def accepted(test):
+    d = oc.GOLDEN / test
+    out = {}
+    if (d / "core_0_output.txt").exists():
+        out[test] = d
+    for r in sorted(d.glob("run_*")):
+        out[r.name] = r
+    return {name: [(p / f"core_{n}_output.txt").read_text() for n in range(4)] for name, p in out.items()}
+
+
+def dumps(outcome, n=4):
+    return [oc.dump_node(outcome, k) for k in range(n)]
+
+
+def components(trace, lens, n):
+    """Nodes that can exchange messages: linked through the home node of every
+    address a node touches (requests, replies, forwards, INVs and evictions all
+    travel between a node and the homes of addresses in some trace)."""
+    parent = list(range(n))
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+
+    for t in range(n):
+        for w in trace[t, :lens[t]]:
+            h = (int(w) >> 12) & 7
+            parent[find(t)] = find(h)
+    groups = collections.defaultdict(list)
+    for t in range(n):
+        groups[find(t)].append(t)
+    return list(groups.values())
+
+
+@pytest.mark.parametrize("test", TESTS)
+def test_lockstep_replay_matches_engine(test):
+    tr, lens = oc.load_test_dir(oc.GOLDEN / test)
+    res = oc.run_system(tr, lens)
+    rep, steps = oc.replay_lockstep(tr, lens)
+    assert rep.digest == res.digest and steps > 0
+    assert dumps(rep) == [oc.dump_node(res, k) for k in range(4)]
+
+
+def test_lockstep_replay_random_systems():
+    rng = np.random.default_rng(3)
+    for N, CS in [(2, 1), (4, 4), (8, 2), (8, 4)]:
+        for _ in range(25):
+            L = int(rng.integers(1, 12))
+            tr = np.zeros((N, L), np.uint16)
+            lens = rng.integers(0, L + 1, size=N).astype(np.uint32)
+            for t in range(N):
+                for i in range(L):
+                    w = rng.random() < 0.5
+                    a = (int(rng.integers(0, N)) << 4) | int(rng.integers(0, 16))
+                    tr[t, i] = oc.pack("W" if w else "R", a, int(rng.integers(0, 256)) if w else 0)
+            res = oc.run_system(tr, lens, num_procs=N, cache_size=CS)
+            rep, _ = oc.replay_lockstep(tr, lens, num_procs=N, cache_size=CS)
+            assert rep.digest == res.digest
+
+
+def test_sample_outcome_set_is_exactly_two():
+    tr, lens = oc.load_test_dir(oc.GOLDEN / "sample")
+    outs, states, complete = oc.explore(tr, lens, max_states=100_000)
+    assert complete and len(outs) == 2
+    expected = accepted("sample")["sample"]
+    assert expected in [dumps(o) for o in outs]
+    lock = oc.run_system(tr, lens)
+    assert lock.digest in [o.digest for o in outs]
+
+
+@pytest.mark.parametrize("test", ["test_1", "test_2"])
+def test_self_message_tests_have_one_outcome(test):
+    """Every node of test_1/test_2 only touches its own addresses: the system
+    splits into independent single-node components, each explored exhaustively;
+    the product of their outcome sets is exactly the expected dump."""
+    tr, lens = oc.load_test_dir(oc.GOLDEN / test)
+    comps = components(tr, lens, 4)
+    assert sorted(map(len, comps)) == [1, 1, 1, 1]
+    final = [None] * 4
+    for comp in comps:
+        sub = np.where(np.isin(np.arange(4), comp)[:, None], tr, 0).astype(np.uint16)
+        sub_lens = np.where(np.isin(np.arange(4), comp), lens, 0).astype(np.uint32)
+        outs, states, complete = oc.explore(sub, sub_lens, max_states=2_000_000)
+        assert complete and len(outs) == 1, (comp, len(outs), states)
+        for t in comp:
+            final[t] = oc.dump_node(outs[0], t)
+    assert final == accepted(test)[test]
+
+
+@pytest.mark.parametrize("test,min_run1,must_hit", [("test_3", 0.15, ["run_1", "run_2"]),
+                                                    ("test_4", 0.5, ["run_1", "run_2"])])
+def test_racy_tests_random_legal_schedules(test, min_run1, must_hit):
+    tr, lens = oc.load_test_dir(oc.GOLDEN / test)
+    acc = accepted(test)
+    hits = collections.Counter()
+    for seed in range(20000):
+        d = dumps(oc.random_schedule(tr, lens, seed))
+        name = next((k for k, v in acc.items() if v == d), None)
+        hits[name] += 1
+    assert hits["run_1"] / 20000 > min_run1
+    for r in must_hit:
+        assert hits[r] > 0, dict(hits)
+    # and the lockstep schedule (the GPU engine's) is run_1
+    lock = oc.run_system(tr, lens)
+    assert [oc.dump_node(lock, k) for k in range(4)] == acc["run_1"]
+
+
+def test_small_systems_exhaustive_contains_lockstep():
+    rng = np.random.default_rng(11)
+    for _ in range(30):
+        N = int(rng.integers(2, 4))
+        L = int(rng.integers(1, 4))
+        tr = np.zeros((N, L), np.uint16)
+        for t in range(N):
+            for i in range(L):
+                w = rng.random() < 0.6
+                a = (int(rng.integers(0, N)) << 4) | int(rng.integers(0, 2))
+                tr[t, i] = oc.pack("W" if w else "R", a, int(rng.integers(1, 256)) if w else 0)
+        lens = np.full(N, L, np.uint32)
+        outs, _, complete = oc.explore(tr, lens, num_procs=N, cache_size=1, max_states=500_000)
+        assert complete
+        lock = oc.run_system(tr, lens, num_procs=N, cache_size=1)
+        assert lock.digest in [o.digest for o in outs]

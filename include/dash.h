@@ -51,6 +51,7 @@ extern "C" {
 #define DASH_EDEVICE -5  /* HIP runtime error (no device, launch failure, ...) */
 #define DASH_ENOMEM -6
 #define DASH_ESTATE -7   /* call out of order (e.g. read_state before run) */
+#define DASH_ETRUNC -8   /* an event log reached its capacity: later events were not kept */
 
 /* per-system protocol fault bits (reference UB made defined) */
 #define DASH_ERR_OVERFLOW 1u  /* receiver queue (256) full: dropped (ref :754-761) */
@@ -80,7 +81,8 @@ typedef struct dash_cfg {
     uint64_t num_systems; /* independent systems in the batch */
     uint64_t max_rounds;  /* per-system round cap; 0 = 1024 + 256*max_instr */
     int32_t device;       /* HIP device ordinal */
-    uint32_t _reserved;
+    uint32_t trace_events; /* per-node event log capacity for DEBUG_MSG / DEBUG_INSTR
+                              emission (ref :179-182, :649-652); 0 = no log */
 } dash_cfg;
 
 /* Final node state in the reference's own terms (processorNode, ref :89-95). */
@@ -121,6 +123,17 @@ typedef struct dash_gen {
     uint32_t _reserved;
 } dash_gen;
 
+/* One logged step of one node (cfg.trace_events > 0), in lockstep order. */
+#define DASH_EV_MSG 0u   /* handled a message: word = message word (type[3:0], sender[6:4],
+                            address[15:8], value|bitVector[23:16], secondReceiver[26:24]) */
+#define DASH_EV_INSTR 1u /* issued an instruction: word = packed instruction */
+typedef struct dash_event {
+    uint32_t round;
+    uint32_t node;
+    uint32_t kind;
+    uint32_t word;
+} dash_event;
+
 typedef struct dash_ctx dash_t;
 
 /* ---- lifecycle / device path (libdash.so, HIP) ---- */
@@ -138,6 +151,9 @@ int dash_read_state(dash_t *h, uint64_t sys, dash_node_state *out /* [num_procs]
 int dash_read_results(dash_t *h, uint64_t first, uint64_t count, uint64_t *digests,
                       uint32_t *rounds, uint32_t *errors);
 int dash_read_hist(dash_t *h, uint64_t sys, uint32_t *hist /* [DASH_NUM_TXN] */);
+/* The event log of one system, merged in lockstep order (round, then node): up to
+   cap events into out, the total into *n. DASH_ETRUNC if a node's log overflowed. */
+int dash_read_events(dash_t *h, uint64_t sys, dash_event *out, uint32_t cap, uint32_t *n);
 /* HIP stream the engine launches on (hipStream_t as void*) */
 void *dash_stream(dash_t *h);
 
@@ -156,6 +172,10 @@ int dash_dump_node(const dash_node_state *s, uint32_t node_id, uint32_t cache_si
 int dash_dump_file(const dash_node_state *s, uint32_t node_id, uint32_t cache_size,
                    const char *path);
 uint64_t dash_digest_node(const dash_node_state *s, uint32_t node_id, uint32_t cache_size);
+/* One event as the reference prints it: DEBUG_MSG "Processor %d msg from: %d, type: %d,
+   address: 0x%02X" (ref :180-181) or DEBUG_INSTR "Processor %d: instr type=%c,
+   address=0x%02X, value=%hhu" (ref :650-651), newline included. Returns bytes or < 0. */
+int dash_format_event(const dash_event *e, char *buf, size_t cap);
 /* main() end to end for one system: parse dir, run on the GPU, write
    core_<n>_output.txt into out_dir (ref :126-739, :860). */
 int dash_simulate_dir(const char *dir, uint32_t num_procs, uint32_t cache_size,

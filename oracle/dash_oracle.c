@@ -69,7 +69,7 @@ typedef struct {
 } onode;
 
 typedef struct {
-    int N, CS, ring;
+    int N, CS, ring, log_msgs;
     onode node[ORC_MAX_PROCS];
     orc_result *res;
     char *log;
@@ -120,6 +120,10 @@ static void handle_message(osys *sy, int tid, omsg msg) {
     omsg r = {0};
 
     sy->res->hist[msg.type]++;
+    if (sy->log && sy->log_msgs && sy->log_len + 64 < sy->log_cap) /* DEBUG_MSG (ref :180-181) */
+        sy->log_len += (uint64_t)snprintf(sy->log + sy->log_len, sy->log_cap - sy->log_len,
+                                          "Processor %d msg from: %d, type: %d, address: 0x%02X\n", tid,
+                                          msg.sender, msg.type, msg.address);
     switch (msg.type) {
     case READ_REQUEST: /* ref :191-237 */
         if (nd->dirState[memBlockAddr] == EM) {
@@ -424,6 +428,7 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
     sy->N = N;
     sy->CS = CS;
     sy->ring = cfg->ring_depth;
+    sy->log_msgs = cfg->log_msgs;
     sy->res = out;
     sy->log = log;
     sy->log_cap = log ? log_cap : 0;

@@ -219,3 +219,59 @@ def test_device_generator_matches_host(dash, kind, loc):
     assert np.array_equal(err, ref["errors"])
     assert stats["hist"] == ref["hist"].tolist()
     assert stats["instructions"] == ref["instructions"]
+
+
+@pytest.mark.parametrize("test", TESTS)
+def test_debug_trace_matches_oracle(dash, test):
+    """DEBUG_MSG / DEBUG_INSTR emission (ref :179-182, :649-652) for a batch of one:
+    the engine's event log, formatted, equals the oracle's lockstep log; tracing
+    does not change the result."""
+    tr, lens = load_test_dir(GOLDEN / test)
+    _, log = run_system(tr, lens, log=True, log_msgs=True)
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, keep_state=True, trace_events=256) as eng:
+        eng.load_traces(tr[None], lens[None])
+        eng.run()
+        ev = eng.read_events(0)
+        assert dash.format_events(ev) == log
+        assert dash.format_events(ev, kinds=(dash.EV_INSTR,)) == run_system(tr, lens, log=True)[1]
+        dig = eng.read_results()[0][0]
+    assert int(dig) == run_system(tr, lens).digest
+
+
+def test_debug_trace_random_batch(dash):
+    rng = np.random.default_rng(21)
+    packed, lens = random_batch(rng, 24, 8, 40)
+    with dash.Engine(24, num_procs=8, cache_size=2, max_instr=40, trace_events=512) as eng:
+        eng.load_traces(packed, lens)
+        eng.run()
+        for s in range(24):
+            _, log = run_system(packed[s], lens[s], num_procs=8, cache_size=2, log=True, log_msgs=True)
+            assert dash.format_events(eng.read_events(s)) == log, s
+
+
+def test_debug_trace_truncation_is_reported(dash):
+    tr, lens = load_test_dir(GOLDEN / "test_4")
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4) as eng:
+        eng.load_traces(tr[None], lens[None])
+        eng.run()
+        with pytest.raises(dash.DashError):
+            eng.read_events(0)
+
+
+def test_cli_debug_flags(dash, tmp_path):
+    exe = dash.PKG / "cache_simulator"
+    (tmp_path / "tests").mkdir()
+    shutil.copytree(GOLDEN / "sample", tmp_path / "tests" / "sample")
+    p = subprocess.run([str(exe), "sample", "--debug-instr", "--debug-msg"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    tr, lens = load_test_dir(GOLDEN / "sample")
+    _, log = run_system(tr, lens, log=True, log_msgs=True)
+    lines = p.stdout.splitlines()
+    assert lines[:4] == [f"Processor {n} initialized" for n in range(4)]
+    assert "\n".join(lines[4:]) + "\n" == log
+    assert [l for l in lines if "instr type" in l] == \
+        [l for l in (GOLDEN / "sample" / "instruction_order.txt").read_text().splitlines() if l.strip()]
+    for n in range(4):
+        assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
+            (GOLDEN / "sample" / f"core_{n}_output.txt").read_bytes()

@@ -33,6 +33,8 @@ struct dash_ctx {
     unsigned long long* d_stats = nullptr;
     uint32_t* d_list[2] = {nullptr, nullptr};  // overflow hand-off lists (ping-pong)
     uint32_t* d_count = nullptr;
+    uint32_t* d_events = nullptr;       // [(sys*N+node)*trace_events][2]
+    uint32_t* d_event_count = nullptr;  // [sys*N+node]
     uint64_t tier_systems[dash::NUM_TIERS] = {};  // systems run per queue-depth tier, last run
     int auto_tier = 0;                         // adaptive first tier
     bool loaded = false;
@@ -83,6 +85,8 @@ static void release(dash_t* h) {
     (void)hipFree(h->d_list[0]);
     (void)hipFree(h->d_list[1]);
     (void)hipFree(h->d_count);
+    (void)hipFree(h->d_events);
+    (void)hipFree(h->d_event_count);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -141,6 +145,12 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     chk(hipMalloc(&h->d_list[1], std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(list)");
     chk(hipMalloc(&h->d_count, 2 * sizeof(uint32_t)), "hipMalloc(count)");
     if (cfg->num_systems > 0xFFFFFFFFull) rc = fail(h, DASH_EINVAL, "more than 2^32 systems");
+    if (cfg->trace_events) {
+        if ((double)nsys * N * cfg->trace_events * 8.0 > 64.0 * (1ull << 30))
+            rc = fail(h, DASH_EINVAL, "event log larger than 64 GiB");
+        chk(hipMalloc(&h->d_events, std::max<uint64_t>(nsys * N * cfg->trace_events, 1) * 8), "hipMalloc(events)");
+        chk(hipMalloc(&h->d_event_count, std::max<uint64_t>(nsys * N, 1) * 4), "hipMalloc(event_count)");
+    }
     if (cfg->flags & DASH_KEEP_STATE)
         chk(hipMalloc(&h->d_state, std::max<uint64_t>(nsys * N, 1) * (16 + CS) * sizeof(uint32_t)),
             "hipMalloc(state)");
@@ -231,6 +241,9 @@ int dash_run(dash_t* h, dash_stats* stats) {
     a.state = h->d_state;
     a.hist = h->d_hist;
     a.keep = (h->cfg.flags & DASH_KEEP_STATE) ? 1u : 0u;
+    a.event_cap = h->cfg.trace_events;
+    a.events = h->d_events;
+    a.event_count = h->d_event_count;
     a.stats = h->d_stats;
     const uint64_t spw = 64 / h->seg;
     HIPCHK(h, hipSetDevice(h->cfg.device));
@@ -352,6 +365,49 @@ int dash_read_hist(dash_t* h, uint64_t sys, uint32_t* hist) {
                              h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return DASH_OK;
+}
+
+int dash_read_events(dash_t* h, uint64_t sys, dash_event* out, uint32_t cap, uint32_t* n) {
+    if (!h || (!out && cap) || !n) return DASH_EINVAL;
+    if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
+    if (!h->d_events) return fail(h, DASH_ESTATE, "created with trace_events = 0");
+    if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
+    const uint32_t N = h->cfg.num_procs, E = h->cfg.trace_events;
+    std::vector<uint32_t> cnt(N), ev((size_t)N * E * 2);
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    HIPCHK(h, hipMemcpyAsync(cnt.data(), h->d_event_count + sys * N, N * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(ev.data(), h->d_events + sys * N * E * 2, ev.size() * 4, hipMemcpyDeviceToHost,
+                             h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    // merge the per-node logs (each in round order) by (round, node): a node logs at
+    // most one event per round, so this is the lockstep order
+    std::vector<uint32_t> pos(N, 0);
+    bool trunc = false;
+    uint64_t total = 0;
+    for (uint32_t t = 0; t < N; t++) {
+        total += cnt[t];
+        if (cnt[t] > E) trunc = true;
+    }
+    uint32_t k = 0;
+    for (;;) {
+        int best = -1;
+        for (uint32_t t = 0; t < N; t++) {
+            if (pos[t] >= std::min(cnt[t], E)) continue;
+            if (best < 0 || ev[((size_t)t * E + pos[t]) * 2] < ev[((size_t)best * E + pos[best]) * 2]) best = (int)t;
+        }
+        if (best < 0) break;
+        const uint32_t* e = &ev[((size_t)best * E + pos[best]) * 2];
+        if (k < cap) {
+            out[k].round = e[0];
+            out[k].node = (uint32_t)best;
+            out[k].kind = (e[1] & 0x80000000u) ? DASH_EV_INSTR : DASH_EV_MSG;
+            out[k].word = e[1] & 0x7FFFFFFFu;
+        }
+        ++k;
+        ++pos[best];
+    }
+    *n = (uint32_t)std::min<uint64_t>(total, 0xFFFFFFFFull);
+    return trunc ? fail(h, DASH_ETRUNC, "event log truncated at %u events per node", E) : DASH_OK;
 }
 
 int dash_load_dir(dash_t* h, const char* dir, uint64_t sys) {

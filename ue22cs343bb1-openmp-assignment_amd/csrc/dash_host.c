@@ -180,6 +180,20 @@ static uint64_t fmix64(uint64_t k) {
     return k;
 }
 
+int dash_format_event(const dash_event *e, char *buf, size_t cap) {
+    if (!e || !buf) return DASH_EINVAL;
+    int n;
+    if (e->kind == DASH_EV_MSG) /* DEBUG_MSG (ref :180-181) */
+        n = snprintf(buf, cap, "Processor %u msg from: %u, type: %u, address: 0x%02X\n", e->node,
+                     (e->word >> 4) & 7u, e->word & 15u, (e->word >> 8) & 0xFFu);
+    else if (e->kind == DASH_EV_INSTR) /* DEBUG_INSTR (ref :650-651) */
+        n = snprintf(buf, cap, "Processor %u: instr type=%c, address=0x%02X, value=%u\n", e->node,
+                     (e->word & 0x8000u) ? 'W' : 'R', (e->word >> 8) & 0x7Fu, e->word & 0xFFu);
+    else
+        return DASH_EINVAL;
+    return (n < 0 || (size_t)n >= cap) ? DASH_EINVAL : n;
+}
+
 uint64_t dash_digest_node(const dash_node_state *s, uint32_t node_id, uint32_t cache_size) {
     uint64_t h = 0x243F6A8885A308D3ULL ^ ((uint64_t)node_id << 56);
     for (int b = 0; b < DASH_MEM_SIZE; b++)

@@ -147,6 +147,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     uint32_t pc = 0, waiting = 0, last_val = 0;
     uint32_t err = 0, maxd = 0, drops = 0;  // maxd in ring-slot bytes until the end
     uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
+    uint32_t nev = 0;         // events logged (DEBUG_MSG / DEBUG_INSTR emission, off unless a.events)
     const uint32_t cap = a.max_rounds;
 
     uint32_t r = 0;
@@ -218,6 +219,17 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         const uint32_t e16 = *ent;
         const uint32_t c16 = *cac;
         const uint32_t mty = m & 15u;
+        if (a.events) {  // wave-uniform: the batch-of-1 trace (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652)
+            COLD();
+            if (has_msg | do_issue) {
+                if (nev < a.event_cap) {
+                    uint32_t* e = a.events + ((sys * N + t) * a.event_cap + nev) * 2;
+                    e[0] = r;
+                    e[1] = has_msg ? m : (ins | 0x80000000u);
+                }
+                ++nev;
+            }
+        }
         if (has_msg)  // messages handled per transactionType, per system
             __hip_atomic_fetch_add(&lds[L::HST + mty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -421,6 +433,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         a.errors[sys] = serr;
     }
     if (live && t == 0 && handoff) a.ovf_list[atomicAdd(a.ovf_count, 1u)] = (uint32_t)sys;
+    if (a.events && report) a.event_count[sys * N + t] = nev;
     maxd >>= 8;  // ring-slot bytes -> messages
     if (a.state && report) {
         uint32_t* st = a.state + (sys * N + t) * (16 + CS);

@@ -36,7 +36,8 @@ TXN_NAMES = ("READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID"
              "UPGRADE", "WRITEBACK_INV", "WRITEBACK_INT", "FLUSH", "FLUSH_INVACK",
              "EVICT_SHARED", "EVICT_MODIFIED")
 
-OK, EINVAL, EIO, EPARSE, EADDR, EDEVICE, ENOMEM, ESTATE = 0, -1, -2, -3, -4, -5, -6, -7
+OK, EINVAL, EIO, EPARSE, EADDR, EDEVICE, ENOMEM, ESTATE, ETRUNC = 0, -1, -2, -3, -4, -5, -6, -7, -8
+EV_MSG, EV_INSTR = 0, 1
 ERR_OVERFLOW, ERR_OOB, ERR_CTZ0, ERR_DEADLOCK, ERR_ROUNDCAP = 1, 2, 4, 8, 16
 KEEP_STATE = 1
 TIER_FROM_32, TIER_FROM_256 = 2, 4
@@ -47,7 +48,8 @@ GEN_UNIFORM, GEN_CONTENTION, GEN_LOCALITY = 0, 1, 2
 EXPORTS = ("dash_create", "dash_destroy", "dash_last_error", "dash_load_traces", "dash_generate",
            "dash_run", "dash_read_state", "dash_read_results", "dash_read_hist", "dash_stream",
            "dash_parse_core_file", "dash_resolve_dir", "dash_load_dir", "dash_init_node_state",
-           "dash_dump_node", "dash_dump_file", "dash_digest_node", "dash_simulate_dir")
+           "dash_dump_node", "dash_dump_file", "dash_digest_node", "dash_simulate_dir",
+           "dash_read_events", "dash_format_event")
 
 
 class DashError(RuntimeError):
@@ -60,7 +62,12 @@ class Cfg(ctypes.Structure):
     _fields_ = [("num_procs", ctypes.c_uint32), ("cache_size", ctypes.c_uint32),
                 ("max_instr", ctypes.c_uint32), ("flags", ctypes.c_uint32),
                 ("num_systems", ctypes.c_uint64), ("max_rounds", ctypes.c_uint64),
-                ("device", ctypes.c_int32), ("_reserved", ctypes.c_uint32)]
+                ("device", ctypes.c_int32), ("trace_events", ctypes.c_uint32)]
+
+
+class Event(ctypes.Structure):
+    _fields_ = [("round", ctypes.c_uint32), ("node", ctypes.c_uint32), ("kind", ctypes.c_uint32),
+                ("word", ctypes.c_uint32)]
 
 
 class NodeState(ctypes.Structure):
@@ -129,6 +136,8 @@ def lib() -> ctypes.CDLL:
         "dash_digest_node": (u64, [ctypes.POINTER(NodeState), u32, u32]),
         "dash_simulate_dir": (i32, [ctypes.c_char_p, u32, u32, u32, ctypes.c_char_p, i32,
                                     ctypes.POINTER(Stats)]),
+        "dash_read_events": (i32, [vp, u64, vp, u32, ctypes.POINTER(u32)]),
+        "dash_format_event": (i32, [ctypes.POINTER(Event), ctypes.c_char_p, ctypes.c_size_t]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -178,6 +187,18 @@ def digest_node(state: NodeState, node_id: int, cache_size=4) -> int:
     return int(lib().dash_digest_node(ctypes.byref(state), node_id, cache_size))
 
 
+def format_events(events, kinds=(0, 1)) -> str:
+    """Lines exactly as the reference prints them under -D DEBUG_MSG / -D DEBUG_INSTR."""
+    buf = ctypes.create_string_buffer(128)
+    out = []
+    for e in events:
+        if e.kind in kinds:
+            n = lib().dash_format_event(ctypes.byref(e), buf, 128)
+            _check(n if n < 0 else OK, "dash_format_event")
+            out.append(buf.value.decode())
+    return "".join(out)
+
+
 def simulate_dir(test_dir, out_dir=".", num_procs=4, cache_size=4, max_instr=32, device=0) -> dict:
     """main() end to end for one trace directory (assignment.c:126-739)."""
     st = Stats()
@@ -193,9 +214,9 @@ class Engine:
     """One batch of independent N-node systems on one GPU (a dash_t handle)."""
 
     def __init__(self, num_systems, num_procs=8, cache_size=4, max_instr=32, keep_state=False,
-                 device=0, max_rounds=0, flags=0):
+                 device=0, max_rounds=0, flags=0, trace_events=0):
         self.cfg = Cfg(num_procs, cache_size, max_instr, (KEEP_STATE if keep_state else 0) | flags,
-                       num_systems, max_rounds, device, 0)
+                       num_systems, max_rounds, device, trace_events)
         self.h = ctypes.c_void_p()
         _check(lib().dash_create(ctypes.byref(self.cfg), ctypes.byref(self.h)), "dash_create")
         self.num_systems = num_systems
@@ -258,6 +279,14 @@ class Engine:
         _check(lib().dash_read_results(self.h, first, count, d.ctypes.data, r.ctypes.data,
                                        e.ctypes.data), "dash_read_results", self.h)
         return d, r, e
+
+    def read_events(self, sys: int) -> list:
+        """The system's DEBUG_MSG / DEBUG_INSTR events in lockstep order (needs trace_events)."""
+        cap = self.cfg.trace_events * self.num_procs
+        arr = (Event * max(cap, 1))()
+        n = ctypes.c_uint32()
+        _check(lib().dash_read_events(self.h, sys, arr, cap, ctypes.byref(n)), "dash_read_events", self.h)
+        return list(arr[:min(n.value, cap)])
 
     def stream(self) -> int:
         return int(lib().dash_stream(self.h) or 0)

@@ -165,6 +165,14 @@ int dash_parse_core_file(const char *path, uint32_t num_procs, uint32_t max_inst
    directory that directly holds core_<n>.txt. Writes the resolved path. */
 int dash_resolve_dir(const char *dir, char *resolved, size_t cap);
 int dash_load_dir(dash_t *h, const char *dir, uint64_t sys);
+/* Bulk ingest: system k = trace directory dirs[k] (same rules as dash_load_dir, ref
+   :822-850; parsed on host threads, no "initialized" lines); n == cfg.num_systems. */
+int dash_load_dirs(dash_t *h, const char *const *dirs, uint64_t n);
+/* Bulk emission: one system's printProcessorState files (ref :853-905) into out_dir
+   (created if missing; needs DASH_KEEP_STATE), and a text file with one line
+   "system digest(hex) rounds errors(hex)" for every system. */
+int dash_dump_system(dash_t *h, uint64_t sys, const char *out_dir);
+int dash_write_digests(dash_t *h, const char *path);
 void dash_init_node_state(dash_node_state *s, uint32_t node_id, uint32_t cache_size);
 /* printProcessorState byte-exact (ref :853-905). Returns bytes written, or < 0. */
 int dash_dump_node(const dash_node_state *s, uint32_t node_id, uint32_t cache_size, char *buf,

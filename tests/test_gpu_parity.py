@@ -275,3 +275,45 @@ def test_cli_debug_flags(dash, tmp_path):
     for n in range(4):
         assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
             (GOLDEN / "sample" / f"core_{n}_output.txt").read_bytes()
+
+
+def test_bulk_dirs_ingest_and_dump(dash, tmp_path):
+    """Trace-directory ingest at scale (ref :822-850 per directory) and bulk
+    printProcessorState emission: 40 directories in one batch."""
+    dirs = [GOLDEN / TESTS[k % 5] for k in range(40)]
+    with dash.Engine(40, num_procs=4, cache_size=4, max_instr=32, keep_state=True) as eng:
+        eng.load_dirs(dirs)
+        eng.run()
+        for k in (0, 1, 2, 3, 4, 37, 39):
+            eng.dump_system(k, tmp_path / str(k))
+            exp = expected_dir(TESTS[k % 5])
+            for n in range(4):
+                assert (tmp_path / str(k) / f"core_{n}_output.txt").read_bytes() == \
+                    (exp / f"core_{n}_output.txt").read_bytes(), (k, n)
+        eng.write_digests(tmp_path / "digests.txt")
+    rows = (tmp_path / "digests.txt").read_text().split("\n")
+    for k in range(40):
+        tr, lens = load_test_dir(GOLDEN / TESTS[k % 5])
+        sysid, dig, rounds, err = rows[k].split()
+        assert int(sysid) == k and int(dig, 16) == run_system(tr, lens).digest
+
+
+def test_cli_batch_and_synthetic(dash, tmp_path):
+    exe = dash.PKG / "cache_simulator"
+    lst = tmp_path / "dirs.txt"
+    lst.write_text("\n".join(str(GOLDEN / t) for t in TESTS) + "\n")
+    p = subprocess.run([str(exe), "--batch", str(lst), "-o", str(tmp_path / "out"), "--digests",
+                        str(tmp_path / "d.txt")], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    for k, t in enumerate(TESTS):
+        for n in range(4):
+            assert (tmp_path / "out" / str(k) / f"core_{n}_output.txt").read_bytes() == \
+                (expected_dir(t) / f"core_{n}_output.txt").read_bytes()
+    p = subprocess.run([str(exe), "--synthetic", "96", "--len", "64", "--kind", "contention", "--digests",
+                        str(tmp_path / "s.txt"), "--dump", "3,95", "-o", str(tmp_path / "syn")],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    ref = run_batch(0x5EED, 0, 96, num_procs=8, cache_size=4, length=64, kind=1, threads=4)
+    got = [int(r.split()[1], 16) for r in (tmp_path / "s.txt").read_text().split("\n") if r]
+    assert got == [int(x) for x in ref["digests"]]
+    assert (tmp_path / "syn" / "95" / "core_7_output.txt").exists()

@@ -12,10 +12,18 @@
  *   --debug-instr / --debug-msg  print the reference's DEBUG_INSTR (:650-651) /
  *       DEBUG_MSG (:180-181) lines to stdout, in lockstep order (the reference's
  *       -D DEBUG_INSTR / -D DEBUG_MSG builds, README :104)
+ *
+ * Bulk modes (one GPU batch, many systems; dumps go to OUT_DIR/<k>/):
+ *   --batch LIST        system k = the k-th trace directory listed in LIST (one per line)
+ *   --synthetic COUNT   COUNT generated systems: --len L (4096) --kind uniform|contention|
+ *                       locality --locality P (0.5) --seed S (0x5EED) --dump K[,K...]
+ *   --digests FILE      "system digest rounds errors" for every system
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/stat.h>
 
 #include "dash.h"
 
@@ -63,12 +71,110 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
     return rc;
 }
 
+typedef struct {
+    unsigned n, cs, m, len, kind, locality;
+    unsigned long long seed;
+    int dev, show;
+    const char *out, *digests, *dump;
+} bulk_opts;
+
+static void print_stats(const dash_stats *st);
+
+static int finish_bulk(dash_t *h, const bulk_opts *o, const dash_stats *st, uint64_t count, int dump_all) {
+    int rc = DASH_OK;
+    if (o->digests) rc = dash_write_digests(h, o->digests);
+    if (rc == DASH_OK && (dump_all || o->dump)) {
+        mkdir(o->out, 0755);
+        const char *p = o->dump;
+        for (uint64_t k = 0; rc == DASH_OK && (dump_all ? k < count : (p && *p)); k++) {
+            uint64_t sys = dump_all ? k : strtoull(p, (char **)&p, 0);
+            if (!dump_all && *p == ',') p++;
+            char dir[4200];
+            snprintf(dir, sizeof dir, "%s/%llu", o->out, (unsigned long long)sys);
+            rc = dash_dump_system(h, sys, dir);
+        }
+    }
+    if (rc != DASH_OK) fprintf(stderr, "%s\n", dash_last_error(h));
+    if (o->show) print_stats(st);
+    return rc;
+}
+
+static int run_batch_list(const char *list, const bulk_opts *o) {
+    FILE *f = fopen(list, "r");
+    if (!f) {
+        fprintf(stderr, "Error: could not open %s\n", list);
+        return DASH_EIO;
+    }
+    char **dirs = NULL, line[4096];
+    uint64_t n = 0, cap = 0;
+    while (fgets(line, sizeof line, f)) {
+        size_t l = strcspn(line, "\r\n");
+        line[l] = 0;
+        if (!l || line[0] == '#') continue;
+        if (n == cap) {
+            cap = cap ? 2 * cap : 64;
+            dirs = (char **)realloc(dirs, cap * sizeof *dirs);
+        }
+        dirs[n++] = strdup(line);
+    }
+    fclose(f);
+    dash_cfg cfg = {0};
+    cfg.num_procs = o->n;
+    cfg.cache_size = o->cs;
+    cfg.max_instr = o->m;
+    cfg.flags = DASH_KEEP_STATE;
+    cfg.num_systems = n;
+    cfg.device = o->dev;
+    dash_t *h = NULL;
+    dash_stats st;
+    int rc = n ? dash_create(&cfg, &h) : DASH_EINVAL;
+    if (rc == DASH_OK && (rc = dash_load_dirs(h, (const char *const *)dirs, n)) == DASH_OK &&
+        (rc = dash_run(h, &st)) == DASH_OK)
+        rc = finish_bulk(h, o, &st, n, 1);
+    else if (h)
+        fprintf(stderr, "%s\n", dash_last_error(h));
+    dash_destroy(h);
+    for (uint64_t k = 0; k < n; k++) free(dirs[k]);
+    free(dirs);
+    return rc;
+}
+
+static int run_synthetic(uint64_t count, const bulk_opts *o) {
+    dash_cfg cfg = {0};
+    cfg.num_procs = o->n;
+    cfg.cache_size = o->cs;
+    cfg.max_instr = o->len;
+    cfg.flags = o->dump ? DASH_KEEP_STATE : 0;
+    cfg.num_systems = count;
+    cfg.device = o->dev;
+    dash_gen g = {0};
+    g.seed = o->seed;
+    g.kind = o->kind;
+    g.locality = o->locality;
+    g.len = o->len;
+    dash_t *h = NULL;
+    dash_stats st;
+    int rc = dash_create(&cfg, &h);
+    if (rc == DASH_OK && (rc = dash_generate(h, &g)) == DASH_OK && (rc = dash_run(h, &st)) == DASH_OK) {
+        printf("%llu systems, %llu instructions, %.3f ms, %.4g instr/s\n", (unsigned long long)st.systems,
+               (unsigned long long)st.instructions, st.kernel_ms, st.instructions / (st.kernel_ms * 1e-3));
+        rc = finish_bulk(h, o, &st, count, 0);
+    } else if (h) {
+        fprintf(stderr, "%s\n", dash_last_error(h));
+    }
+    dash_destroy(h);
+    return rc;
+}
+
 int main(int argc, char *argv[]) {
     unsigned n = 4, cs = 4, m = 32;
-    int dev = 0, show = 0, dbg_instr = 0, dbg_msg = 0;
-    const char *out = ".", *dir = NULL;
+    int dev = 0, show = 0, dbg_instr = 0, dbg_msg = 0, n_given = 0;
+    const char *out = ".", *dir = NULL, *batch = NULL, *digests = NULL, *dump = NULL;
+    unsigned long long synth = 0, seed = 0x5EED;
+    unsigned len = 4096, kind = DASH_GEN_UNIFORM;
+    double loc = 0.5;
     for (int i = 1; i < argc; i++) {
-        if (!strcmp(argv[i], "-n") && i + 1 < argc) n = (unsigned)atoi(argv[++i]);
+        if (!strcmp(argv[i], "-n") && i + 1 < argc) n = (unsigned)atoi(argv[++i]), n_given = 1;
         else if (!strcmp(argv[i], "-c") && i + 1 < argc) cs = (unsigned)atoi(argv[++i]);
         else if (!strcmp(argv[i], "-m") && i + 1 < argc) m = (unsigned)atoi(argv[++i]);
         else if (!strcmp(argv[i], "-o") && i + 1 < argc) out = argv[++i];
@@ -76,7 +182,26 @@ int main(int argc, char *argv[]) {
         else if (!strcmp(argv[i], "-s")) show = 1;
         else if (!strcmp(argv[i], "--debug-instr")) dbg_instr = 1;
         else if (!strcmp(argv[i], "--debug-msg")) dbg_msg = 1;
+        else if (!strcmp(argv[i], "--batch") && i + 1 < argc) batch = argv[++i];
+        else if (!strcmp(argv[i], "--synthetic") && i + 1 < argc) synth = strtoull(argv[++i], NULL, 0);
+        else if (!strcmp(argv[i], "--digests") && i + 1 < argc) digests = argv[++i];
+        else if (!strcmp(argv[i], "--dump") && i + 1 < argc) dump = argv[++i];
+        else if (!strcmp(argv[i], "--len") && i + 1 < argc) len = (unsigned)atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = strtoull(argv[++i], NULL, 0);
+        else if (!strcmp(argv[i], "--locality") && i + 1 < argc) loc = atof(argv[++i]);
+        else if (!strcmp(argv[i], "--kind") && i + 1 < argc) {
+            const char *k = argv[++i];
+            kind = !strcmp(k, "contention") ? DASH_GEN_CONTENTION : !strcmp(k, "locality") ? DASH_GEN_LOCALITY
+                                                                                         : DASH_GEN_UNIFORM;
+        }
         else if (!dir) dir = argv[i];
+    }
+    if (batch || synth) {
+        if (synth && !n_given) n = 8; /* synthetic systems default to 8 nodes (BASELINE configs) */
+        bulk_opts o = {n, cs, m, len, kind, (unsigned)(loc * 65536.0), seed, dev, show, out, digests, dump};
+        if (o.locality > 65536u) o.locality = 65536u;
+        int rc = batch ? run_batch_list(batch, &o) : run_synthetic(synth, &o);
+        return rc == DASH_OK ? EXIT_SUCCESS : EXIT_FAILURE;
     }
     if (!dir) {
         fprintf(stderr, "Usage: %s <test_directory>\n", argv[0]); /* ref :128 */
@@ -89,12 +214,14 @@ int main(int argc, char *argv[]) {
         fprintf(stderr, "cache_simulator: failed (%d)\n", rc);
         return EXIT_FAILURE;
     }
-    if (show) {
-        fprintf(stderr, "rounds %llu instructions %llu errors 0x%llx dropped %llu\n",
-                (unsigned long long)st.rounds_total, (unsigned long long)st.instructions,
-                (unsigned long long)st.err_bits, (unsigned long long)st.dropped);
-        for (int k = 0; k < DASH_NUM_TXN; k++)
-            fprintf(stderr, "  %-15s %llu\n", txn_names[k], (unsigned long long)st.hist[k]);
-    }
+    if (show) print_stats(&st);
     return st.err_bits ? 2 : EXIT_SUCCESS;
+}
+
+static void print_stats(const dash_stats *st) {
+    fprintf(stderr, "rounds %llu instructions %llu errors 0x%llx dropped %llu\n",
+            (unsigned long long)st->rounds_total, (unsigned long long)st->instructions,
+            (unsigned long long)st->err_bits, (unsigned long long)st->dropped);
+    for (int k = 0; k < DASH_NUM_TXN; k++)
+        fprintf(stderr, "  %-15s %llu\n", txn_names[k], (unsigned long long)st->hist[k]);
 }

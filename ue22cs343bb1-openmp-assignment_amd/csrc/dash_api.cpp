@@ -5,8 +5,13 @@
 // (:149-155) and the per-thread private processorNode (:145).
 #include <hip/hip_runtime.h>
 
+#include <sys/stat.h>
+
 #include <algorithm>
+#include <atomic>
+#include <cerrno>
 #include <cstdarg>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -426,6 +431,70 @@ int dash_load_dir(dash_t* h, const char* dir, uint64_t sys) {
         printf("Processor %u initialized\n", t); /* ref :850 */
     }
     return dash_load_traces(h, tr.data(), std::max<uint32_t>(M, 1), lens.data(), 1);
+}
+
+int dash_load_dirs(dash_t* h, const char* const* dirs, uint64_t n) {
+    if (!h || (!dirs && n)) return DASH_EINVAL;
+    if (n != h->cfg.num_systems) return fail(h, DASH_EINVAL, "%llu directories for %llu systems",
+                                             (unsigned long long)n, (unsigned long long)h->cfg.num_systems);
+    const uint32_t N = h->cfg.num_procs, M = h->cfg.max_instr, stride = std::max<uint32_t>(M, 1);
+    std::vector<uint16_t> tr((size_t)n * N * stride, 0);
+    std::vector<uint32_t> lens((size_t)n * N, 0);
+    std::atomic<uint64_t> next{0}, bad{~0ull};
+    std::atomic<int> bad_rc{DASH_OK};
+    auto worker = [&]() {
+        char base[4096], path[4200];
+        for (uint64_t k; (k = next.fetch_add(1)) < n;) {
+            int rc = dash_resolve_dir(dirs[k], base, sizeof base);
+            for (uint32_t t = 0; rc == DASH_OK && t < N; t++) {
+                snprintf(path, sizeof path, "%s/core_%u.txt", base, t);
+                rc = dash_parse_core_file(path, N, M, tr.data() + (k * N + t) * stride, &lens[k * N + t]);
+            }
+            if (rc != DASH_OK) {
+                uint64_t prev = bad.load();
+                while (k < prev && !bad.compare_exchange_weak(prev, k)) {
+                }
+                bad_rc = rc;
+            }
+        }
+    };
+    const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({n, 16, std::max(1u, std::thread::hardware_concurrency())}));
+    std::vector<std::thread> pool;
+    for (unsigned i = 1; i < nt; i++) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
+    if (bad.load() != ~0ull)
+        return fail(h, bad_rc.load(), "%s: trace directory rejected (%d)", dirs[bad.load()], bad_rc.load());
+    return dash_load_traces(h, tr.data(), stride, lens.data(), n);
+}
+
+int dash_dump_system(dash_t* h, uint64_t sys, const char* out_dir) {
+    if (!h || !out_dir) return DASH_EINVAL;
+    std::vector<dash_node_state> st(h->cfg.num_procs);
+    int rc = dash_read_state(h, sys, st.data());
+    if (rc != DASH_OK) return rc;
+    if (mkdir(out_dir, 0755) != 0 && errno != EEXIST) return fail(h, DASH_EIO, "mkdir %s", out_dir);
+    for (uint32_t t = 0; t < h->cfg.num_procs; t++) {
+        char path[4200];
+        snprintf(path, sizeof path, "%s/core_%u_output.txt", out_dir, t);
+        rc = dash_dump_file(&st[t], t, h->cfg.cache_size, path);
+        if (rc != DASH_OK) return fail(h, rc, "write %s", path);
+    }
+    return DASH_OK;
+}
+
+int dash_write_digests(dash_t* h, const char* path) {
+    if (!h || !path) return DASH_EINVAL;
+    const uint64_t n = h->cfg.num_systems;
+    std::vector<uint64_t> d(n);
+    std::vector<uint32_t> r(n), e(n);
+    int rc = dash_read_results(h, 0, n, d.data(), r.data(), e.data());
+    if (rc != DASH_OK) return rc;
+    FILE* f = fopen(path, "w");
+    if (!f) return fail(h, DASH_EIO, "open %s", path);
+    for (uint64_t k = 0; k < n; k++)
+        fprintf(f, "%llu %016llx %u %x\n", (unsigned long long)k, (unsigned long long)d[k], r[k], e[k]);
+    return fclose(f) == 0 ? DASH_OK : fail(h, DASH_EIO, "write %s", path);
 }
 
 int dash_simulate_dir(const char* dir, uint32_t num_procs, uint32_t cache_size, uint32_t max_instr,

@@ -49,7 +49,8 @@ EXPORTS = ("dash_create", "dash_destroy", "dash_last_error", "dash_load_traces",
            "dash_run", "dash_read_state", "dash_read_results", "dash_read_hist", "dash_stream",
            "dash_parse_core_file", "dash_resolve_dir", "dash_load_dir", "dash_init_node_state",
            "dash_dump_node", "dash_dump_file", "dash_digest_node", "dash_simulate_dir",
-           "dash_read_events", "dash_format_event")
+           "dash_read_events", "dash_format_event", "dash_load_dirs", "dash_dump_system",
+           "dash_write_digests")
 
 
 class DashError(RuntimeError):
@@ -137,6 +138,9 @@ def lib() -> ctypes.CDLL:
         "dash_simulate_dir": (i32, [ctypes.c_char_p, u32, u32, u32, ctypes.c_char_p, i32,
                                     ctypes.POINTER(Stats)]),
         "dash_read_events": (i32, [vp, u64, vp, u32, ctypes.POINTER(u32)]),
+        "dash_load_dirs": (i32, [vp, ctypes.POINTER(ctypes.c_char_p), u64]),
+        "dash_dump_system": (i32, [vp, u64, ctypes.c_char_p]),
+        "dash_write_digests": (i32, [vp, ctypes.c_char_p]),
         "dash_format_event": (i32, [ctypes.POINTER(Event), ctypes.c_char_p, ctypes.c_size_t]),
     }
     for name, (res, args) in sig.items():
@@ -251,6 +255,17 @@ class Engine:
 
     def load_dir(self, test_dir):
         _check(lib().dash_load_dir(self.h, str(test_dir).encode(), 0), "dash_load_dir", self.h)
+
+    def load_dirs(self, dirs):
+        """Bulk ingest: system k = trace directory dirs[k]."""
+        arr = (ctypes.c_char_p * max(len(dirs), 1))(*[str(d).encode() for d in dirs])
+        _check(lib().dash_load_dirs(self.h, arr, len(dirs)), "dash_load_dirs", self.h)
+
+    def dump_system(self, sys: int, out_dir):
+        _check(lib().dash_dump_system(self.h, sys, str(out_dir).encode()), "dash_dump_system", self.h)
+
+    def write_digests(self, path):
+        _check(lib().dash_write_digests(self.h, str(path).encode()), "dash_write_digests", self.h)
 
     def generate(self, seed, length, kind=GEN_UNIFORM, locality=0, sys_base=0):
         g = Gen(seed, sys_base, kind, locality, length, 0)

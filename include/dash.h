@@ -83,6 +83,9 @@ typedef struct dash_cfg {
     int32_t device;       /* HIP device ordinal */
     uint32_t trace_events; /* per-node event log capacity for DEBUG_MSG / DEBUG_INSTR
                               emission (ref :179-182, :649-652); 0 = no log */
+    uint64_t schedule_seed; /* 0: lowest-sender-first lockstep (the parity schedule); else a
+                               seeded legal schedule: per round a node sits out w.p. 1/4 and
+                               senders deliver in a seeded order */
 } dash_cfg;
 
 /* Final node state in the reference's own terms (processorNode, ref :89-95). */

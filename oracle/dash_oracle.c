@@ -401,6 +401,17 @@ static uint64_t fmix64(uint64_t k) {
     return k;
 }
 
+int orc_arb_stall(uint64_t seed, uint64_t round, uint32_t t) {
+    const uint64_t key = fmix64(seed ^ (round * 0x9E3779B97F4A7C15ULL) ^ 0xD1B54A32D192ED03ULL);
+    return (int)((key >> (8 * t)) & 3u) == 0;
+}
+
+uint32_t orc_arb_prio(uint64_t seed, uint64_t round, uint32_t t, uint32_t P) {
+    const uint64_t key = fmix64(seed ^ (round * 0x9E3779B97F4A7C15ULL));
+    const uint32_t A = ((uint32_t)key & (P - 1)) | 1u, B = (uint32_t)(key >> 8) & (P - 1);
+    return (t * A + B) & (P - 1);
+}
+
 uint64_t orc_digest_node(const orc_node_state *s, int node_id, int cache_size) {
     uint64_t h = 0x243F6A8885A308D3ULL ^ ((uint64_t)node_id << 56);
     for (int b = 0; b < ORC_MEM_SIZE; b++)
@@ -452,10 +463,11 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
         }
         out->rounds++;
 
-        /* every node steps on start-of-round state */
+        /* every node steps on start-of-round state (unless a seeded arbitration stalls it) */
         for (int t = 0; t < N; t++) {
             onode *nd = &sy->node[t];
             nd->nout = 0;
+            if (cfg->arb_seed && orc_arb_stall(cfg->arb_seed, out->rounds - 1, (uint32_t)t)) continue;
             if (nd->qcount > 0) {
                 omsg m = nd->q[nd->head];
                 nd->head = (nd->head + 1) % (uint32_t)sy->ring;
@@ -465,8 +477,20 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
                 issue_instruction(sy, t);
             }
         }
-        /* end-of-round delivery: ascending sender, program order (sendMessage ref :741-765) */
-        for (int s = 0; s < N; s++) {
+        /* end-of-round delivery: ascending sender (or the seeded sender order), program
+           order within a sender (sendMessage ref :741-765) */
+        int order[ORC_MAX_PROCS];
+        for (int s = 0; s < N; s++) order[s] = s;
+        if (cfg->arb_seed) {
+            uint32_t P = 1;
+            while (P < (uint32_t)N) P <<= 1;
+            int k = 0;
+            for (uint32_t pr = 0; pr < P; pr++)
+                for (int s = 0; s < N; s++)
+                    if (orc_arb_prio(cfg->arb_seed, out->rounds - 1, (uint32_t)s, P) == pr) order[k++] = s;
+        }
+        for (int si = 0; si < N; si++) {
+            const int s = order[si];
             onode *src = &sy->node[s];
             for (int k = 0; k < src->nout; k++) {
                 int rcv = src->out_to[k];

@@ -30,7 +30,7 @@ TXN_NAMES = ["READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID"
 class OrcCfg(ctypes.Structure):
     _fields_ = [("num_procs", ctypes.c_int), ("cache_size", ctypes.c_int),
                 ("ring_depth", ctypes.c_int), ("max_rounds", ctypes.c_uint64),
-                ("log_msgs", ctypes.c_int), ("_pad", ctypes.c_int)]
+                ("log_msgs", ctypes.c_int), ("_pad", ctypes.c_int), ("arb_seed", ctypes.c_uint64)]
 
 
 class OrcNodeState(ctypes.Structure):
@@ -135,12 +135,12 @@ def load_test_dir(d, num_procs=4, max_instr=32):
 # ---------------------------------------------------------------- runs
 
 def run_system(trace, lens, num_procs=4, cache_size=4, ring_depth=256, max_rounds=0, log=False,
-               log_msgs=False):
+               log_msgs=False, arb_seed=0):
     """log=True also returns the DEBUG_INSTR lines (plus DEBUG_MSG lines with
     log_msgs=True) in lockstep order (round, then node)."""
     trace = np.ascontiguousarray(trace, dtype=np.uint16)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
-    cfg = OrcCfg(num_procs, cache_size, ring_depth, max_rounds, 1 if log_msgs else 0)
+    cfg = OrcCfg(num_procs, cache_size, ring_depth, max_rounds, 1 if log_msgs else 0, 0, arb_seed)
     res = OrcResult()
     buf = ctypes.create_string_buffer(1 << 20) if log else None
     rc = lib().orc_run_system(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1],

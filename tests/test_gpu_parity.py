@@ -56,10 +56,10 @@ def state_arrays(nodes, N, CS):
     return out
 
 
-def check_batch(dash, packed, lens, N, CS, max_rounds=0, flags=0):
+def check_batch(dash, packed, lens, N, CS, max_rounds=0, flags=0, seed=0):
     nsys = packed.shape[0]
     with dash.Engine(nsys, num_procs=N, cache_size=CS, max_instr=packed.shape[2], keep_state=True,
-                     max_rounds=max_rounds, flags=flags) as eng:
+                     max_rounds=max_rounds, flags=flags, schedule_seed=seed) as eng:
         eng.load_traces(packed, lens)
         stats = eng.run()
         dig, rnd, err = eng.read_results()
@@ -68,7 +68,7 @@ def check_batch(dash, packed, lens, N, CS, max_rounds=0, flags=0):
         instr_total = 0
         for s in range(nsys):
             res = run_system(packed[s], lens[s], num_procs=N, cache_size=CS, ring_depth=256,
-                             max_rounds=max_rounds or (1024 + 256 * packed.shape[2]))
+                             max_rounds=max_rounds or (1024 + 256 * packed.shape[2]), arb_seed=seed)
             gpu_nodes = eng.read_state(s)
             assert state_arrays(gpu_nodes, N, CS) == state_arrays(res.node, N, CS), f"system {s}"
             assert int(rnd[s]) == res.rounds, f"system {s} rounds"
@@ -317,3 +317,25 @@ def test_cli_batch_and_synthetic(dash, tmp_path):
     got = [int(r.split()[1], 16) for r in (tmp_path / "s.txt").read_text().split("\n") if r]
     assert got == [int(x) for x in ref["digests"]]
     assert (tmp_path / "syn" / "95" / "core_7_output.txt").exists()
+
+
+@pytest.mark.parametrize("seed,N,CS", [(1, 8, 4), (87, 4, 4), (0xABCDEF, 8, 2), (5, 3, 1)])
+def test_seeded_schedule_bit_exact(dash, seed, N, CS):
+    """Seeded legal schedules (stalls + seeded sender order): bit-exact vs the
+    oracle's twin (orc_arb_stall / orc_arb_prio), including contention."""
+    rng = np.random.default_rng(seed)
+    packed, lens = random_batch(rng, 96, N, 48, hot_frac=0.3)
+    check_batch(dash, packed, lens, N, CS, seed=seed)
+
+
+def test_seeded_schedule_reaches_other_accepted_run(dash, tmp_path):
+    """test_4 accepts run_1..run_4 (test4.sh); lockstep gives run_1, the seeded
+    schedule 87 gives run_2 -- both legal serialisations."""
+    tr, lens = load_test_dir(GOLDEN / "test_4")
+    with dash.Engine(2, num_procs=4, cache_size=4, max_instr=32, keep_state=True, schedule_seed=87) as eng:
+        eng.load_traces(np.stack([tr, tr]), np.stack([lens, lens]))
+        eng.run()
+        eng.dump_system(1, tmp_path)
+    for n in range(4):
+        assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
+            (GOLDEN / "test_4" / "run_2" / f"core_{n}_output.txt").read_bytes()

@@ -148,3 +148,29 @@ def test_small_systems_exhaustive_contains_lockstep():
         assert complete
         lock = oc.run_system(tr, lens, num_procs=N, cache_size=1)
         assert lock.digest in [o.digest for o in outs]
+
+
+def test_seeded_schedules_are_legal():
+    """The engine's seeded schedules (stalls + seeded sender order) land inside
+    the exhaustively enumerated legal outcome sets."""
+    tr, lens = oc.load_test_dir(oc.GOLDEN / "sample")
+    outs, _, complete = oc.explore(tr, lens, max_states=100_000)
+    legal = {o.digest for o in outs}
+    assert complete
+    for seed in range(1, 200):
+        assert oc.run_system(tr, lens, arb_seed=seed).digest in legal
+    rng = np.random.default_rng(17)
+    for _ in range(20):
+        N, L = int(rng.integers(2, 4)), int(rng.integers(1, 4))
+        tr = np.zeros((N, L), np.uint16)
+        for t in range(N):
+            for i in range(L):
+                w = rng.random() < 0.6
+                a = (int(rng.integers(0, N)) << 4) | int(rng.integers(0, 2))
+                tr[t, i] = oc.pack("W" if w else "R", a, int(rng.integers(1, 256)) if w else 0)
+        lens = np.full(N, L, np.uint32)
+        outs, _, complete = oc.explore(tr, lens, num_procs=N, cache_size=1, max_states=500_000)
+        assert complete
+        legal = {o.digest for o in outs}
+        for seed in range(1, 40):
+            assert oc.run_system(tr, lens, num_procs=N, cache_size=1, arb_seed=seed).digest in legal

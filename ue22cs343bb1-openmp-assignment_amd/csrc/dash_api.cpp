@@ -247,6 +247,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
     a.hist = h->d_hist;
     a.keep = (h->cfg.flags & DASH_KEEP_STATE) ? 1u : 0u;
     a.event_cap = h->cfg.trace_events;
+    a.arb_seed = h->cfg.schedule_seed;
     a.events = h->d_events;
     a.event_count = h->d_event_count;
     a.stats = h->d_stats;

@@ -49,6 +49,7 @@ struct SimArgs {
     uint32_t* events;         // [(sys*N+node)*event_cap][2]: round, word (bit 31: issued instruction)
     uint32_t* event_count;    // [sys*N+node] events produced (may exceed event_cap)
     unsigned long long* stats;  // [STAT_WORDS]
+    uint64_t arb_seed;        // 0: lowest-sender-first lockstep; else the seeded schedule
 };
 
 struct GenArgs {

@@ -77,7 +77,10 @@ __device__ __forceinline__ uint64_t vote(bool c) { return __builtin_amdgcn_ballo
 // keeps a rarely taken branch a branch (no if-conversion onto the common path)
 #define COLD() asm volatile("" ::: "memory")
 
-template <int P, int CS, uint32_t RING>
+// ARB: seeded legal schedule -- per round, a node sits out with
+// probability 1/4 and senders deliver in a seeded affine order (oracle twins:
+// orc_arb_stall, orc_arb_prio); otherwise every node steps, lowest sender first
+template <int P, int CS, uint32_t RING, bool ARB>
 __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     using L = Lds<P, CS, RING>;
     constexpr uint32_t SPW = 64 / P;
@@ -201,12 +204,24 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         }
 
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
-        const bool has_msg = cq != 0;
+        bool stall = false;
+        uint32_t bitI = 1u << (4 * t);
+        if constexpr (ARB) {  // round keys are wave-uniform: computed on the scalar unit
+            const uint64_t rk = a.arb_seed ^ ((uint64_t)r * 0x9E3779B97F4A7C15ull);
+            const uint64_t key = fmix64(rk), skey = fmix64(rk ^ 0xD1B54A32D192ED03ull);
+            stall = ((skey >> (8 * t)) & 3u) == 0;
+            const uint32_t A = ((uint32_t)key & (P - 1)) | 1u, Bc = (uint32_t)(key >> 8) & (P - 1);
+            bitI = 1u << (4 * ((t * A + Bc) & (P - 1)));
+        }
+        const bool has_msg = (cq != 0) & !stall;
         const uint32_t m = *reinterpret_cast<const uint32_t*>(ldsb + L::RNG * 4 + ((tq - cq) & RMASK) + lane * 4);
         const uint32_t ins = lds16[L::WND * 2 + (pc % (WIN * CHUNK)) * 64 + sw];
-        const bool do_issue = !has_msg & can_issue;
+        const bool do_issue = (cq == 0) & can_issue & !stall;
         pc += do_issue ? 1u : 0u;
-        cq = __builtin_elementwise_sub_sat(cq, SLOT);  // pop (cq is a multiple of SLOT)
+        if constexpr (ARB)
+            cq -= has_msg ? SLOT : 0u;
+        else
+            cq = __builtin_elementwise_sub_sat(cq, SLOT);  // pop (cq is a multiple of SLOT)
         // message addresses are < 0x80 (a send to a node >= N is dropped), so bits
         // 14..8 give the address of a message and of an instruction alike
         const uint32_t mw = has_msg ? m : ins;
@@ -350,7 +365,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         // bits below its own, and the receiver's capacity check (ref :754-761)
         // compares the receiver's count plus that rank with the ring depth.
         lds[L::MQ + 2 * lane + 1] = tq | (cq << 8);  // tail byte offset | count << 16
-        const uint32_t bitP = 2u << (4 * t), bitB = 4u << (4 * t), bitI = 1u << (4 * t);
+        const uint32_t bitP = bitI << 1, bitB = bitI << 2;
         if (vP)
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (vB)
@@ -538,7 +553,10 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
 
 template <int P, int CS, uint32_t RING>
 static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t s) {
-    hipLaunchKernelGGL((sim_kernel<P, CS, RING>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+    if (a.arb_seed)
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, true>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, false>), dim3((uint32_t)groups), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

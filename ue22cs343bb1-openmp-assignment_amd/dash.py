@@ -63,7 +63,8 @@ class Cfg(ctypes.Structure):
     _fields_ = [("num_procs", ctypes.c_uint32), ("cache_size", ctypes.c_uint32),
                 ("max_instr", ctypes.c_uint32), ("flags", ctypes.c_uint32),
                 ("num_systems", ctypes.c_uint64), ("max_rounds", ctypes.c_uint64),
-                ("device", ctypes.c_int32), ("trace_events", ctypes.c_uint32)]
+                ("device", ctypes.c_int32), ("trace_events", ctypes.c_uint32),
+                ("schedule_seed", ctypes.c_uint64)]
 
 
 class Event(ctypes.Structure):
@@ -218,9 +219,9 @@ class Engine:
     """One batch of independent N-node systems on one GPU (a dash_t handle)."""
 
     def __init__(self, num_systems, num_procs=8, cache_size=4, max_instr=32, keep_state=False,
-                 device=0, max_rounds=0, flags=0, trace_events=0):
+                 device=0, max_rounds=0, flags=0, trace_events=0, schedule_seed=0):
         self.cfg = Cfg(num_procs, cache_size, max_instr, (KEEP_STATE if keep_state else 0) | flags,
-                       num_systems, max_rounds, device, trace_events)
+                       num_systems, max_rounds, device, trace_events, schedule_seed)
         self.h = ctypes.c_void_p()
         _check(lib().dash_create(ctypes.byref(self.cfg), ctypes.byref(self.h)), "dash_create")
         self.num_systems = num_systems

@@ -88,6 +88,63 @@ def read_profile(kind):
     return None
 
 
+def timed_runs(eng, args, world, local_rank):
+    import torch
+    import torch.distributed as dist
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        eng.run()
+    barrier()
+    t0 = time.perf_counter()
+    stats = None
+    for _ in range(args.steps):
+        stats = eng.run()
+    barrier()
+    return time.perf_counter() - t0, stats
+
+
+def sweep(args, dash, rank, world, local_rank):
+    """configs[4]: 8M systems over 8 GPUs (args.systems per GPU), CACHE_SIZE x
+    locality grid; one RCCL all-reduce of the transaction histograms per point."""
+    import torch
+    import torch.distributed as dist
+    M = args.systems
+    sys_base, M = shard(rank, world, M)
+    points = []
+    for cs in (1, 2, 4, 8, 16):
+        for p in (0.0, 0.25, 0.5, 0.75, 1.0):
+            eng = dash.Engine(M, num_procs=8, cache_size=cs, max_instr=args.len, device=local_rank)
+            eng.generate(args.seed, args.len, kind=dash.GEN_LOCALITY, locality=int(round(p * 65536)),
+                         sys_base=sys_base)
+            elapsed, stats = timed_runs(eng, args, world, local_rank)
+            elapsed, totals = reduce_totals(
+                elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
+                                          stats["dropped"]], torch.device("cuda", local_rank), world)
+            eng.close()
+            points.append({"cache_size": cs, "locality": p,
+                           "value": world * M * 8 * args.len * args.steps / elapsed,
+                           "ms_per_step": elapsed / args.steps * 1e3,
+                           "rounds_per_system": totals[14] / (world * M),
+                           "hist": totals[:13], "err_systems": totals[15],
+                           "tier_systems": stats["tier_systems"]})
+    if rank == 0:
+        print(json.dumps({"metric": "simulated instr/sec (whole node), 8-core DASH systems; sweep",
+                          "unit": "instr/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "higher_is_better": True, "scaling": "weak", "dtype": "u8",
+                          "data": "synthetic locality traces (on-device generator, seed keyed by global id)",
+                          "config": {"workload": f"{world * M} systems ({M}/GPU) x 8 nodes x {args.len} "
+                                                 f"instr, CACHE_SIZE x locality grid",
+                                     "parallelism": f"systems sharded over {world} GPU(s)"},
+                          "sweep": points}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,6 +161,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--first-depth", type=int, choices=[0, 32, 256], default=0,
                     help="first queue-depth tier (0 = adaptive, starting at 16)")
+    ap.add_argument("--sweep", action="store_true",
+                    help="BASELINE configs[4]: CACHE_SIZE {1,2,4,8,16} x locality {0,.25,.5,.75,1}, "
+                         "systems sharded over the ranks, histograms all-reduced per configuration")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -117,6 +177,9 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    if args.sweep:
+        return sweep(args, dash, rank, world, local_rank)
 
     kind = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
             "locality": dash.GEN_LOCALITY}[args.kind]
@@ -185,7 +248,7 @@ def main():
             "valu_issue": ({"achieved": prof["valu_per_launch"] / avg_kernel_s,
                             "peak": VALU_PEAK, "unit": "wave-instr/s",
                             "frac": prof["valu_per_launch"] / avg_kernel_s / VALU_PEAK,
-                            "valu_per_round": prof.get("valu_per_wave_round"),
+                            "valu_per_wave_round": prof["valu_per_launch"] / max(stats["wave_rounds"], 1),
                             "source": prof.get("source")} if prof else None),
             "cpu_baseline": cpu,
             "kernel_ms_avg": avg_kernel_s * 1e3,

@@ -13,7 +13,7 @@ kind, out = sys.argv[1], sys.argv[2]
 agg = collections.defaultdict(float)
 dur = {}
 for d in sys.argv[3:]:
-    for f in glob.glob(f"{d}/**/*.csv", recursive=True):
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
             if "sim_kernel<8, 4, 16" not in row["Kernel_Name"]:
                 continue

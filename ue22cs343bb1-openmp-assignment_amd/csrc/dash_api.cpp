@@ -176,7 +176,7 @@ int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const u
     for (uint64_t i = 0; i < num_systems * N; i++)
         if (lens[i] > h->cfg.max_instr || lens[i] > stride)
             return fail(h, DASH_EINVAL, "trace %llu longer than max_instr", (unsigned long long)i);
-    // lane-interleaved layout: [group][chunk][lane][8 x u16]
+    // lane-contiguous layout: [group][lane][chunk][4 x u16]
     const uint64_t words = h->groups * (uint64_t)h->nchunks * 64;
     constexpr uint32_t C = dash::CHUNK_INSTR;
     std::vector<uint16_t> host(words * C, 0);
@@ -190,7 +190,7 @@ int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const u
                 if (((w >> 12) & 7u) >= N)
                     return fail(h, DASH_EADDR, "system %llu node %u: address 0x%02X homed on node >= %u",
                                 (unsigned long long)s, t, (w >> 8) & 0x7F, N);
-                host[((g * h->nchunks + i / C) * 64 + lane0 + t) * C + (i % C)] = w;
+                host[((g * 64 + lane0 + t) * h->nchunks + i / C) * C + (i % C)] = w;
             }
         }
     }

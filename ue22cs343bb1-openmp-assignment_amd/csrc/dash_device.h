@@ -28,7 +28,7 @@ enum : uint32_t {
 };
 
 struct SimArgs {
-    const uint2* trace;       // [group][chunk][64] x 8 B (4 packed instructions)
+    const uint2* trace;       // [group][64 lanes][chunk] x 8 B (4 packed instructions)
     const uint32_t* lens;     // [sys * N + node]
     uint64_t nsys;
     uint32_t nchunks;

@@ -18,13 +18,16 @@
 //     scratch with deeper queues, the last tier being the reference's 256
 //     (MSG_BUFFER_SIZE, ref :9). The schedule is deterministic, so a system that
 //     never fills its queues is identical at every depth;
-//   * traces stream from HBM in a lane-interleaved layout [group][chunk][lane]
-//     (4 instructions = 8 B per lane-chunk) into a 3-chunk LDS window, refilled
+//   * traces stream from HBM in a lane-contiguous layout [group][lane][chunk]
+//     (4 instructions = 8 B per lane-chunk; one lane's stream is contiguous, so
+//     each fetched line is consumed by the same lane over its next refills)
+//     into a 2-chunk LDS window with one chunk pending in registers, refilled
 //     every 4 rounds, so no global-load latency sits on a round's critical path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "dash_device.h"
 
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     uint32_t cst = 0xFFFFFFFFu;  // CS x INVALID
 
     // trace window prefill: chunks 0..WIN-1 landed, chunk WIN pending in registers
-    const uint2* tr = a.trace + ((sys / SPW) * a.nchunks) * 64 + (sys % SPW) * P + t;
+    const uint2* tr = a.trace + ((sys / SPW) * 64 + (sys % SPW) * P + t) * a.nchunks;
     const uint32_t nch = (len + CHUNK - 1) / CHUNK;
     // instruction i of a lane lives in window row i % (WIN*CHUNK)
     auto put_chunk = [&](uint32_t c, uint2 v) {
@@ -137,10 +140,10 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     };
 #pragma unroll
     for (uint32_t c = 0; c < WIN; ++c)
-        if (c < nch) put_chunk(c, tr[c * 64]);
+        if (c < nch) put_chunk(c, tr[c]);
     uint32_t pend_idx = WIN;
     uint2 pend = make_uint2(0, 0);
-    if (pend_idx < nch) pend = tr[pend_idx * 64];
+    if (pend_idx < nch) pend = tr[pend_idx];
 
     // this node's incoming queue (messageBuffer, ref :81-87): tail and count of
     // its LDS ring in ring-slot bytes (x SLOT), owned by the node; senders learn
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
             if (pend_idx < nch && pend_idx < pc / CHUNK + WIN) {
                 put_chunk(pend_idx, pend);
                 ++pend_idx;
-                if (pend_idx < nch) pend = tr[pend_idx * 64];
+                if (pend_idx < nch) pend = tr[pend_idx];
             }
         }
 
@@ -507,10 +510,12 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
     const uint64_t N = g.num_procs;
     for (uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
          gid += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t lane = (uint32_t)(gid & 63u);
-        const uint64_t rest = gid >> 6;
-        const uint32_t chunk = (uint32_t)(rest % g.nchunks);
-        const uint64_t group = rest / g.nchunks;
+        // lane-contiguous layout [group][lane][chunk]: consecutive threads write
+        // consecutive chunks of one lane's stream
+        const uint32_t chunk = (uint32_t)(gid % g.nchunks);
+        const uint64_t rest = gid / g.nchunks;
+        const uint32_t lane = (uint32_t)(rest & 63u);
+        const uint64_t group = rest >> 6;
         const uint32_t t = lane % P;
         const uint64_t sys = group * (64u / P) + lane / P;
         const bool live = sys < g.nsys && t < g.num_procs;
@@ -551,12 +556,21 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
     }
 }
 
+// occupancy experiments only (tools/): DASH_LDS_PAD adds dynamic LDS per workgroup
+static uint32_t lds_pad() {
+    static const uint32_t pad = [] {
+        const char* e = getenv("DASH_LDS_PAD");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    return pad;
+}
+
 template <int P, int CS, uint32_t RING>
 static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t s) {
     if (a.arb_seed)
-        hipLaunchKernelGGL((sim_kernel<P, CS, RING, true>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, true>), dim3((uint32_t)groups), dim3(64), lds_pad(), s, a);
     else
-        hipLaunchKernelGGL((sim_kernel<P, CS, RING, false>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, false>), dim3((uint32_t)groups), dim3(64), lds_pad(), s, a);
     return hipGetLastError();
 }
 

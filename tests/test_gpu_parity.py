@@ -339,3 +339,32 @@ def test_seeded_schedule_reaches_other_accepted_run(dash, tmp_path):
     for n in range(4):
         assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
             (GOLDEN / "test_4" / "run_2" / f"core_{n}_output.txt").read_bytes()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_full_size_sampled_parity(dash, kind):
+    """BASELINE configs[2] (uniform) and [3] (contention) at full size: 1M systems x
+    8 nodes x 4096 instructions, CACHE_SIZE 4 (64 GiB of trace). Size-independent
+    properties: every instruction issued, per-system statistics consistent with the
+    totals, a run started one queue-depth tier deeper gives the same digest of every
+    system (checksum of checksums), and 48 sampled systems are bit-exact (digest,
+    rounds, error bits) against the oracle."""
+    N, CS, L, nsys, seed = 8, 4, 4096, 1 << 20, 0x5EED
+    runs = []
+    for flags in (0, dash.TIER_FROM_32):
+        with dash.Engine(nsys, num_procs=N, cache_size=CS, max_instr=L, flags=flags) as eng:
+            eng.generate(seed, L, kind=kind)
+            st = eng.run()
+            runs.append((st, eng.read_results()))
+    (st, (dig, rnd, err)), (st2, (dig2, rnd2, err2)) = runs
+    assert st["systems"] == nsys and st["instructions"] == nsys * N * L
+    assert st["rounds_total"] == int(rnd.sum()) and int(rnd.min()) > 0
+    assert st["err_systems"] == int(np.count_nonzero(err))
+    assert np.array_equal(dig, dig2) and np.array_equal(rnd, rnd2) and np.array_equal(err, err2)
+    assert st["hist"] == st2["hist"]
+    rng = np.random.default_rng(kind)
+    for s in sorted(rng.choice(nsys, 48, replace=False).tolist()):
+        ref = run_batch(seed, s, 1, num_procs=N, cache_size=CS, length=L, kind=kind, threads=1)
+        assert int(dig[s]) == int(ref["digests"][0]), f"system {s} digest"
+        assert int(rnd[s]) == int(ref["rounds"][0]), f"system {s} rounds"
+        assert int(err[s]) == int(ref["errors"][0]), f"system {s} errors"

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "dash_device.h"
 
@@ -42,8 +43,23 @@ enum : uint32_t {
 enum : uint32_t { ST_M = 0, ST_E = 1, ST_S = 2, ST_I = 3 };  // cacheLineState (ref :17)
 enum : uint32_t { D_EM = 0, D_S = 1, D_U = 2 };              // directoryEntryState (ref :28)
 
+#ifndef DASH_WCHUNK
+#define DASH_WCHUNK 4
+#endif
 constexpr uint32_t WIN = 2;        // trace window chunks per lane (enough: see the refill)
-constexpr uint32_t CHUNK = 4;      // instructions per chunk (8 B)
+constexpr uint32_t CHUNK = CHUNK_INSTR;   // instructions per 8-B HBM trace chunk (layout unit)
+constexpr uint32_t WCHUNK = DASH_WCHUNK;  // instructions per window refill (2: 4-B, 4: 8-B loads)
+static_assert(WCHUNK == 2 || WCHUNK == 4, "window chunk");
+using wchunk_t = typename std::conditional<WCHUNK == 4, uint2, uint32_t>::type;
+#ifndef DASH_QCHECK
+#define DASH_QCHECK 4              // rounds between quiescence votes (a multiple of WCHUNK)
+#endif
+#ifndef DASH_MASKED_STORE
+#define DASH_MASKED_STORE 0
+#endif
+#ifndef DASH_WAVES_PER_EU
+#define DASH_WAVES_PER_EU 0
+#endif
 
 // message word (ref `message`, :70-79, 20 B -> 4 B):
 //   [3:0] type  [6:4] sender  [15:8] address  [23:16] value | bitVector
@@ -67,13 +83,16 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t ENT = 0;                      // u16 [16][64]  mem | bitVector<<8   (swizzled)
     static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8      (swizzled)
     static constexpr uint32_t RNG = CAC + CS * 64 / 2;      // u32 [RING][64] message words
-    static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*CHUNK][64] trace window  (swizzled)
+    static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
     static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
-    static constexpr uint32_t HST = WND + WIN * CHUNK * 64 / 2;  // u32 [13][64/P+1] per-system counters
+    static constexpr uint32_t HST = WND + WIN * WCHUNK * 64 / 2;  // u32 [13][64/P+1] per-system counters
     static constexpr uint32_t MQ = (HST + 13 * HSTRIDE + 1) & ~1u;  // u32 [64][2] arrivals mask, tail|count<<16
     static constexpr uint32_t DUM = MQ + 2 * 64;            // u32 [64]      target of a suppressed store
-    static constexpr uint32_t WORDS = DUM + 64;
+    static constexpr uint32_t WORDS = DUM + (DASH_MASKED_STORE ? 0 : 64);
 };
+
+__device__ __forceinline__ void chunk_words(uint2 v, uint32_t& x, uint32_t& y) { x = v.x; y = v.y; }
+__device__ __forceinline__ void chunk_words(uint32_t v, uint32_t& x, uint32_t& y) { x = v; y = 0; }
 
 // wave-wide vote without HIP's int round trip (bool -> 0/1 -> compare)
 __device__ __forceinline__ uint64_t vote(bool c) { return __builtin_amdgcn_ballot_w64(c); }
@@ -84,7 +103,11 @@ __device__ __forceinline__ uint64_t vote(bool c) { return __builtin_amdgcn_ballo
 // probability 1/4 and senders deliver in a seeded affine order (oracle twins:
 // orc_arb_stall, orc_arb_prio); otherwise every node steps, lowest sender first
 template <int P, int CS, uint32_t RING, bool ARB>
-__global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
+__global__ __launch_bounds__(64)
+#if DASH_WAVES_PER_EU
+__attribute__((amdgpu_waves_per_eu(DASH_WAVES_PER_EU)))
+#endif
+void sim_kernel(const SimArgs a) {
     using L = Lds<P, CS, RING>;
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
@@ -128,21 +151,27 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
     uint32_t cst = 0xFFFFFFFFu;  // CS x INVALID
 
     // trace window prefill: chunks 0..WIN-1 landed, chunk WIN pending in registers
-    const uint2* tr = a.trace + ((sys / SPW) * 64 + (sys % SPW) * P + t) * a.nchunks;
-    const uint32_t nch = (len + CHUNK - 1) / CHUNK;
-    // instruction i of a lane lives in window row i % (WIN*CHUNK)
-    auto put_chunk = [&](uint32_t c, uint2 v) {
-        uint16_t* const w = lds16 + L::WND * 2 + ((c % WIN) * CHUNK) * 64 + sw;
-        w[0] = (uint16_t)v.x;
-        w[64] = (uint16_t)(v.x >> 16);
-        w[128] = (uint16_t)v.y;
-        w[192] = (uint16_t)(v.y >> 16);
+    // one lane's stream is contiguous (layout unit: 8-B chunks of 4), read in WCHUNK pieces
+    const wchunk_t* tr = reinterpret_cast<const wchunk_t*>(
+        a.trace + ((sys / SPW) * 64 + (sys % SPW) * P + t) * a.nchunks);
+    const uint32_t nch = (len + WCHUNK - 1) / WCHUNK;
+    // instruction i of a lane lives in window row i % (WIN*WCHUNK)
+    auto put_chunk = [&](uint32_t c, wchunk_t v) {
+        uint16_t* const w = lds16 + L::WND * 2 + ((c % WIN) * WCHUNK) * 64 + sw;
+        uint32_t x, y;
+        chunk_words(v, x, y);
+        w[0] = (uint16_t)x;
+        w[64] = (uint16_t)(x >> 16);
+        if constexpr (WCHUNK == 4) {
+            w[128] = (uint16_t)y;
+            w[192] = (uint16_t)(y >> 16);
+        }
     };
 #pragma unroll
     for (uint32_t c = 0; c < WIN; ++c)
         if (c < nch) put_chunk(c, tr[c]);
     uint32_t pend_idx = WIN;
-    uint2 pend = make_uint2(0, 0);
+    wchunk_t pend{};
     if (pend_idx < nch) pend = tr[pend_idx];
 
     // this node's incoming queue (messageBuffer, ref :81-87): tail and count of
@@ -181,17 +210,18 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         }
 
         // ---- wave-uniform housekeeping: trace window refill ----
-        // Invariant at a refill point: pend_idx >= pc/CHUNK + 1 and the window holds
-        // chunks pend_idx-2 and pend_idx-1. pc advances <= CHUNK per CHUNK rounds, so
-        // the chunks read until the next refill point (pc/CHUNK, pc/CHUNK + 1) are
-        // always resident; the pending chunk's load has CHUNK rounds to land.
-        if ((r & (CHUNK - 1)) == 0) {
-            // quiescence is absorbing, so testing it every CHUNK rounds only adds
+        // Invariant at a refill point: pend_idx >= pc/WCHUNK + 1 and the window holds
+        // chunks pend_idx-2 and pend_idx-1. pc advances <= WCHUNK per WCHUNK rounds, so
+        // the chunks read until the next refill point (pc/WCHUNK, pc/WCHUNK + 1) are
+        // always resident; the pending chunk's load has WCHUNK rounds to land.
+        if ((r & (WCHUNK - 1)) == 0) {
+            // quiescence is absorbing, so testing it every QCHECK rounds only adds
             // idle rounds (no state changes, not counted in `rounds`)
-            if (vote(active) == 0) break;
+            const bool qpoint = (r & (DASH_QCHECK - 1)) == 0;
+            if (qpoint && vote(active) == 0) break;
             // a non-final tier stops a system soon after its first overflow: it will be
             // re-simulated from scratch at the next depth, its results here are void
-            if constexpr (!FINAL) {
+            if (!FINAL && qpoint) {
                 const uint64_t ovf = vote(maxd > RING * SLOT);
                 if (ovf != 0 && ((uint32_t)(ovf >> seg) & SEGMASK) != 0) {
                     cq = 0;
@@ -199,7 +229,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
                     waiting = 0;
                 }
             }
-            if (pend_idx < nch && pend_idx < pc / CHUNK + WIN) {
+            if (pend_idx < nch && pend_idx < pc / WCHUNK + WIN) {
                 put_chunk(pend_idx, pend);
                 ++pend_idx;
                 if (pend_idx < nch) pend = tr[pend_idx];
@@ -218,7 +248,7 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
         }
         const bool has_msg = (cq != 0) & !stall;
         const uint32_t m = *reinterpret_cast<const uint32_t*>(ldsb + L::RNG * 4 + ((tq - cq) & RMASK) + lane * 4);
-        const uint32_t ins = lds16[L::WND * 2 + (pc % (WIN * CHUNK)) * 64 + sw];
+        const uint32_t ins = lds16[L::WND * 2 + (pc % (WIN * WCHUNK)) * 64 + sw];
         const bool do_issue = (cq == 0) & can_issue & !stall;
         pc += do_issue ? 1u : 0u;
         if constexpr (ARB)
@@ -387,14 +417,22 @@ __global__ __launch_bounds__(64) void sim_kernel(const SimArgs a) {
             const uint32_t off = ((q.y + (rank << 8)) & RMASK) | ((seg + d) * 4);
             if constexpr (FINAL) {
                 const bool ok = v & ((q.y >> 16) + rank < RING);
+#if DASH_MASKED_STORE
+                if (ok) *reinterpret_cast<uint32_t*>(ldsb + L::RNG * 4 + off) = w;
+#else
                 *reinterpret_cast<uint32_t*>(ldsb + (ok ? L::RNG * 4 + off : L::DUM * 4 + lane * 4)) = w;
+#endif
                 if (vote(v & !ok) != 0) {
                     COLD();
                     err |= (v & !ok) ? DASH_ERR_OVERFLOW_D : 0u;
                     drops += (v & !ok) ? 1u : 0u;
                 }
             } else {
+#if DASH_MASKED_STORE
+                if (v) *reinterpret_cast<uint32_t*>(ldsb + L::RNG * 4 + off) = w;
+#else
                 *reinterpret_cast<uint32_t*>(ldsb + (v ? L::RNG * 4 + off : L::DUM * 4 + lane * 4)) = w;
+#endif
             }
         };
         place(vP, dP, bitP, wP);

@@ -26,7 +26,8 @@ import subprocess
 import numpy as np
 
 PKG = pathlib.Path(__file__).resolve().parent
-LIB_PATH = PKG / "libdash.so"
+# DASH_LIB: an alternative build of the same library (kernel variant experiments, tools/)
+LIB_PATH = pathlib.Path(os.environ["DASH_LIB"]) if os.environ.get("DASH_LIB") else PKG / "libdash.so"
 
 MEM_SIZE = 16
 MAX_PROCS = 8

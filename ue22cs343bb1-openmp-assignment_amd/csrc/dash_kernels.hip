@@ -179,27 +179,37 @@ void sim_kernel(const SimArgs a) {
     // them through MQ each round. Below the final depth the count is not clamped:
     // exceeding RING is the overflow that hands the system to the next depth.
     uint32_t cq = 0, tq = 0;
-    uint32_t pc = 0, waiting = 0, last_val = 0;
+    uint32_t pc = 0, last_val = 0;
+    // waitingForReply (ref :157) of every lane as one wave mask: updated by the scalar
+    // unit, read per lane through inverse_ballot (no VALU)
+    uint64_t wmask = 0;
     uint32_t err = 0, maxd = 0, drops = 0;  // maxd in ring-slot bytes until the end
     uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
     uint32_t nev = 0;         // events logged (DEBUG_MSG / DEBUG_INSTR emission, off unless a.events)
     const uint32_t cap = a.max_rounds;
+
+    const uint32_t wES = T_ES | (t << 4), wEM = T_EMOD | (t << 4);  // eviction notice, sender part
+    // the queue tail a node publishes carries its own ring column (lane * 4 B) in
+    // the bits below the slot: a sender's slot address is tail + rank slots, masked
+    const uint32_t col = lane * 4u;
 
     uint32_t r = 0;
     for (;; ++r) {
         // ---- quiescence / round cap, on start-of-round state ----
         // A system is active while any of its nodes has a message or can issue;
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
-        bool can_issue = (waiting == 0) & (pc < len);
+        const bool waiting = __builtin_amdgcn_inverse_ballot_w64(wmask);
+        bool can_issue = !waiting & (pc < len);
         bool active = (cq != 0) | can_issue;
         if (r == cap) {  // wave-uniform: every system still active has run `cap` rounds
             COLD();
             const uint64_t act = vote(active);
-            if (((uint32_t)(act >> seg) & SEGMASK) != 0) {
+            const bool kill = ((uint32_t)(act >> seg) & SEGMASK) != 0;
+            wmask &= ~vote(kill);
+            if (kill) {
                 err |= DASH_ERR_ROUNDCAP_D;
                 cq = 0;
                 len = pc;
-                waiting = 0;
                 can_issue = false;
                 active = false;
             }
@@ -223,10 +233,14 @@ void sim_kernel(const SimArgs a) {
             // re-simulated from scratch at the next depth, its results here are void
             if (!FINAL && qpoint) {
                 const uint64_t ovf = vote(maxd > RING * SLOT);
-                if (ovf != 0 && ((uint32_t)(ovf >> seg) & SEGMASK) != 0) {
-                    cq = 0;
-                    len = pc;
-                    waiting = 0;
+                if (ovf != 0) {
+                    COLD();
+                    const bool stop = ((uint32_t)(ovf >> seg) & SEGMASK) != 0;
+                    wmask &= ~vote(stop);
+                    if (stop) {
+                        cq = 0;
+                        len = pc;
+                    }
                 }
             }
             if (pend_idx < nch && pend_idx < pc / WCHUNK + WIN) {
@@ -365,16 +379,16 @@ void sim_kernel(const SimArgs a) {
         const uint32_t srA = (WBINV | WBINT) ? msr : msender;
         const uint32_t wA = mk(tA, t, addr, valA, srA, dsS ? 1u : 0u);
         const uint32_t dE = laddr >> 4;
-        const bool inN = dE < N;
+        const bool inN = laddr < N * 16u;  // home node of the evicted line exists
         const bool vE = ev & inN;
-        const uint32_t wE = (lst == ST_M ? (uint32_t)T_EMOD : (uint32_t)T_ES) | (t << 4) | (c16 << 8);
+        const uint32_t wE = (lst == ST_M ? wEM : wES) | (c16 << 8);
         const bool vP = vA | vE;
         const uint32_t dP = (vA ? dA : dE) & 7u;
         const uint32_t wP = vA ? wA : wE;
         // second copy of a flush: WRITEBACK_INV always (:498), WRITEBACK_INT if sr != home (:281)
         const bool vB = WBINV | (WBINT & (H != msr));
 
-        waiting = ((iR & !hit) | (iW & !own_hit)) ? 1u : ((RRD | RWR | RID | FLUSH | FIA) ? 0u : waiting);
+        wmask = vote((iR & !hit) | (iW & !own_hit)) | (wmask & ~vote(RRD | RWR | RID | FLUSH | FIA));
         last_val = do_issue ? ival : last_val;
         const bool oob = ev & !inN;  // ref UB: messageBuffers[15] -> drop + flag
         if (oob | ctz0) {  // rare: keep the counting off the common path
@@ -397,7 +411,7 @@ void sim_kernel(const SimArgs a) {
         // ref :364-379): a sender's slot is the receiver's tail plus the number of
         // bits below its own, and the receiver's capacity check (ref :754-761)
         // compares the receiver's count plus that rank with the ring depth.
-        lds[L::MQ + 2 * lane + 1] = tq | (cq << 8);  // tail byte offset | count << 16
+        lds[L::MQ + 2 * lane + 1] = tq | col | (cq << 8);  // tail | ring column | count << 16
         const uint32_t bitP = bitI << 1, bitB = bitI << 2;
         if (vP)
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -412,9 +426,10 @@ void sim_kernel(const SimArgs a) {
         auto place = [&](bool v, uint32_t d, uint32_t bit, uint32_t w) {
             const uint2 q = *reinterpret_cast<const uint2*>(&lds[L::MQ + 2 * (seg + d)]);
             const uint32_t rank = (uint32_t)__builtin_popcount(q.x & (bit - 1u));
-            // slot byte offset = receiver tail + rank slots (the count bits above
-            // bit 15 fall off the mask)
-            const uint32_t off = ((q.y + (rank << 8)) & RMASK) | ((seg + d) * 4);
+            // slot byte offset = receiver tail + rank slots, in the receiver's ring
+            // column (bits 7..2, untouched by the add); the count bits above bit 15
+            // fall off the mask
+            const uint32_t off = (q.y + (rank << 8)) & RMASK;
             if constexpr (FINAL) {
                 const bool ok = v & ((q.y >> 16) + rank < RING);
 #if DASH_MASKED_STORE
@@ -453,7 +468,7 @@ void sim_kernel(const SimArgs a) {
     }
 
     // ---- results ----
-    if (waiting) err |= DASH_ERR_DEADLOCK_D;
+    if (__builtin_amdgcn_inverse_ballot_w64(wmask)) err |= DASH_ERR_DEADLOCK_D;
     uint32_t serr = err;
     uint32_t rounds = last_act + 1u;  // ~0 + 1 = 0 for a system that never ran
 #pragma unroll

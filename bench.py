@@ -24,7 +24,12 @@ import time
 ROOT = pathlib.Path(__file__).resolve().parent
 PEAK_HBM = 8.0e12  # B/s, MI355X_MICROARCH.md chip table
 BYTES_PER_INSTR = 2  # packed trace record read once
-VALU_PEAK = 256 * 2.4e9  # wave-instr/s: 256 CUs x 1 VALU issue per cycle x 2.4 GHz
+# VALU issue ceiling for this kernel's instruction forms (v_cndmask_e64, v_cmp_e64, v_bfe,
+# v_or3, v_lshl_or, ...): 1 wave64 instruction per cycle per CU (4 cycles per SIMD),
+# measured by tools/micro (profiles/r01/micro); the SIMD-32 issue limit of plain VOP2
+# forms in homogeneous streams is 2 per cycle per CU. 256 CUs x 2.4 GHz.
+VALU_PEAK = 256 * 2.4e9
+VALU_PEAK_SIMD32 = 2 * VALU_PEAK
 
 
 def load_dash():
@@ -245,10 +250,14 @@ def main():
                          "traffic": prof.get("hbm_bytes_per_launch") if prof else None},
             # the bound that actually binds this integer state machine: VALU issue,
             # one wave-instruction per cycle per CU
-            "valu_issue": ({"achieved": prof["valu_per_launch"] / avg_kernel_s,
+            # VALU issue rate of the first-tier launch, from its own PMC run (count / duration)
+            "valu_issue": ({"achieved": prof["valu_per_launch"] / (prof["kernel_ms"] / 1e3),
                             "peak": VALU_PEAK, "unit": "wave-instr/s",
-                            "frac": prof["valu_per_launch"] / avg_kernel_s / VALU_PEAK,
+                            "frac": prof["valu_per_launch"] / (prof["kernel_ms"] / 1e3) / VALU_PEAK,
+                            "frac_of_simd32_issue": prof["valu_per_launch"] / (prof["kernel_ms"] / 1e3)
+                            / VALU_PEAK_SIMD32,
                             "valu_per_wave_round": prof["valu_per_launch"] / max(stats["wave_rounds"], 1),
+                            "l2_hit_rate": prof.get("l2_hit_rate"),
                             "source": prof.get("source")} if prof else None),
             "cpu_baseline": cpu,
             "kernel_ms_avg": avg_kernel_s * 1e3,

@@ -1,8 +1,7 @@
 #!/bin/bash
 # Round evidence on one MI355X (run from the repo root): GPU parity suite, default bench
 # (with CPU baseline), contention bench, rocprofv3 kernel-trace stats of the bench command,
-# and one rocprofv3 PMC pass per counter group (full-size workload, 1 step each; the
-# contention passes start at the 32-deep tier, where the adaptive bench runs settle).
+# and one rocprofv3 PMC pass per counter group (full-size workload, 1 step each).
 # Usage: tools/evidence.sh TAG        -> gpurun_out/ev_TAG/
 set -uo pipefail
 TAG=$1; OUT=gpurun_out/ev_$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
@@ -20,10 +19,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/trace.log" 2>&1 || exit 1
 pmc() {  # kind name counters...
   local kind=$1 name=$2; shift 2
-  local extra=""; [ "$kind" = contention ] && extra="--first-depth 32"
   step pmc "$kind" "$name"
   timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/pmc_$kind/$name" -o run -- \
-      python3 bench.py --kind "$kind" $extra --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc_$kind/$name.log" 2>&1 \
+      python3 bench.py --kind "$kind" --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc_$kind/$name.log" 2>&1 \
       || { echo "pmc $name failed"; exit 1; }
 }
 for kind in uniform contention; do

@@ -1,38 +1,52 @@
-"""Per-launch summary of the first-tier sim_kernel from rocprofv3 PMC passes
-(FETCH_SIZE, WRITE_SIZE and an SQ pass), written to profiles/pmc_<kind>.json
-and read by bench.py for roofline.traffic and valu_issue.
+"""Per-launch summary of one sim_kernel instantiation from rocprofv3 PMC passes
+(tools/evidence.sh: separate --pmc runs), written to profiles/pmc_<kind>.json and
+read by bench.py for roofline.traffic and valu_issue.
 
-FETCH_SIZE / WRITE_SIZE are in KiB (rocprofv3 derived counters); bytes are
-reported as measured (MI355X_MICROARCH.md: FETCH_SIZE is calibrated only for
-16-B-per-lane streaming reads, which this kernel does not do -- its 8-B trace
-loads are uncalibrated, so the figure is indicative).
-Usage: python tools/pmc_summary.py KIND OUT_JSON DIR [DIR ...]"""
-import collections, csv, glob, json, sys
+HBM bytes, corrected as MI355X_MICROARCH.md (§HBM) prescribes: FETCH_SIZE counts
+TCC_EA0_RDREQ x 64 B, i.e. half of every 128-B request. When the request-size
+counters were collected (tcc1 pass) the read bytes are the size-weighted sum
+RDREQ_128B x 128 + RDREQ_64B x 64 + RDREQ_32B x 32 (disjoint on this part: the
+uniform launch measured RDREQ 3.038e9 = 128B 3.038e9 + 64B 2.5e4 + 32B 0);
+otherwise 2 x FETCH_SIZE. WRITE_SIZE is taken as measured (KiB).
+Usage: python tools/pmc_summary.py KIND KERNEL_SUBSTRING OUT_JSON DIR [DIR ...]"""
+import collections
+import csv
+import glob
+import json
+import sys
 
-kind, out = sys.argv[1], sys.argv[2]
+kind, kname, out = sys.argv[1], sys.argv[2], sys.argv[3]
 agg = collections.defaultdict(float)
 dur = {}
-for d in sys.argv[3:]:
+for d in sys.argv[4:]:
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for row in csv.DictReader(open(f)):
-            if "sim_kernel<8, 4, 16" not in row["Kernel_Name"]:
+            if kname not in row["Kernel_Name"]:
                 continue
             agg[row["Counter_Name"]] += float(row["Counter_Value"])
             dur[row["Counter_Name"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
-res = {"kernel": "dash::sim_kernel<8, 4, 16u>", "workload": kind, "source": " ".join(sys.argv[3:])}
-if "FETCH_SIZE" in agg:
-    res["fetch_bytes_per_launch"] = agg["FETCH_SIZE"] * 1024
+res = {"kernel": kname, "workload": kind, "source": " ".join(sys.argv[4:])}
+for k in sorted(agg):
+    res[k.lower()] = agg[k]
+read = None
+if "TCC_EA0_RDREQ_128B_sum" in agg:
+    r128, r64, r32 = agg["TCC_EA0_RDREQ_128B_sum"], agg.get("TCC_EA0_RDREQ_64B_sum", 0.0), \
+        agg.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+    read = r128 * 128 + r64 * 64 + r32 * 32
+    res["read_bytes_source"] = "TCC_EA0_RDREQ_{128B,64B,32B} size-weighted"
+elif "FETCH_SIZE" in agg:
+    read = agg["FETCH_SIZE"] * 1024 * 2
+    res["read_bytes_source"] = "2 x FETCH_SIZE (128-B requests counted at 64 B)"
+if read is not None:
+    res["read_bytes_per_launch"] = read
 if "WRITE_SIZE" in agg:
     res["write_bytes_per_launch"] = agg["WRITE_SIZE"] * 1024
-if "FETCH_SIZE" in agg and "WRITE_SIZE" in agg:
-    res["hbm_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
-for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"):
-    if k in agg:
-        res[k.lower()] = agg[k]
+if read is not None and "WRITE_SIZE" in agg:
+    res["hbm_bytes_per_launch"] = read + agg["WRITE_SIZE"] * 1024
+if "TCC_HIT_sum" in agg and "TCC_MISS_sum" in agg:
+    res["l2_hit_rate"] = agg["TCC_HIT_sum"] / max(agg["TCC_HIT_sum"] + agg["TCC_MISS_sum"], 1.0)
 if "SQ_INSTS_VALU" in agg:
     res["valu_per_launch"] = agg["SQ_INSTS_VALU"]
     res["kernel_ms"] = dur["SQ_INSTS_VALU"]
-if len(sys.argv) > 4 and "wave_rounds" in res:
-    pass
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

@@ -93,7 +93,7 @@ def read_profile(kind):
     return None
 
 
-def timed_runs(eng, args, world, local_rank):
+def timed_runs(eng, args, world, dev):
     import torch
     import torch.distributed as dist
 
@@ -113,7 +113,7 @@ def timed_runs(eng, args, world, local_rank):
     return time.perf_counter() - t0, stats
 
 
-def sweep(args, dash, rank, world, local_rank):
+def sweep(args, dash, rank, world, dev):
     """configs[4]: 8M systems over 8 GPUs (args.systems per GPU), CACHE_SIZE x
     locality grid; one RCCL all-reduce of the transaction histograms per point."""
     import torch
@@ -123,13 +123,13 @@ def sweep(args, dash, rank, world, local_rank):
     points = []
     for cs in (1, 2, 4, 8, 16):
         for p in (0.0, 0.25, 0.5, 0.75, 1.0):
-            eng = dash.Engine(M, num_procs=8, cache_size=cs, max_instr=args.len, device=local_rank)
+            eng = dash.Engine(M, num_procs=8, cache_size=cs, max_instr=args.len, device=dev)
             eng.generate(args.seed, args.len, kind=dash.GEN_LOCALITY, locality=int(round(p * 65536)),
                          sys_base=sys_base)
-            elapsed, stats = timed_runs(eng, args, world, local_rank)
+            elapsed, stats = timed_runs(eng, args, world, dev)
             elapsed, totals = reduce_totals(
                 elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
-                                          stats["dropped"]], torch.device("cuda", local_rank), world)
+                                          stats["dropped"]], torch.device("cuda", dev), world)
             eng.close()
             points.append({"cache_size": cs, "locality": p,
                            "value": world * M * 8 * args.len * args.steps / elapsed,
@@ -166,6 +166,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--first-depth", type=int, choices=[0, 32, 256], default=0,
                     help="first queue-depth tier (0 = adaptive, starting at 16)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
+                         "1-GPU rehearsal of the distributed path in tests/test_gpu_distributed.py)")
     ap.add_argument("--sweep", action="store_true",
                     help="BASELINE configs[4]: CACHE_SIZE {1,2,4,8,16} x locality {0,.25,.5,.75,1}, "
                          "systems sharded over the ranks, histograms all-reduced per configuration")
@@ -179,12 +182,17 @@ def main():
     import torch.distributed as dist
 
     dash = load_dash()
-    torch.cuda.set_device(local_rank)
+    # one rank per GPU; ranks beyond the visible GPUs share them (rehearsal only)
+    dev = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
 
     if args.sweep:
-        return sweep(args, dash, rank, world, local_rank)
+        return sweep(args, dash, rank, world, dev)
 
     kind = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
             "locality": dash.GEN_LOCALITY}[args.kind]
@@ -192,7 +200,7 @@ def main():
     M = args.systems
     tier_flag = {0: 0, 32: dash.TIER_FROM_32, 256: dash.TIER_FROM_256}[args.first_depth]
     eng = dash.Engine(M, num_procs=8, cache_size=args.cache_size, max_instr=args.len,
-                      device=local_rank, flags=tier_flag)
+                      device=dev, flags=tier_flag)
     sys_base, M = shard(rank, world, M)
     eng.generate(args.seed, args.len, kind=kind, locality=locality, sys_base=sys_base)
 
@@ -215,7 +223,7 @@ def main():
 
     elapsed, totals = reduce_totals(
         elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
-                                  stats["dropped"]], torch.device("cuda", local_rank), world)
+                                  stats["dropped"]], torch.device("cuda", dev), world)
 
     instr_per_step = world * M * 8 * args.len
     value = instr_per_step * args.steps / elapsed

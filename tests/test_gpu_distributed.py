@@ -1,0 +1,50 @@
+"""The distributed bench path on real hardware, rehearsed on one GPU: bench.py under
+torchrun with 2 ranks (both on the box's one GPU, gloo collectives; on an 8-GPU node
+the same code runs one rank per GPU over RCCL). Sharding by global system id, the
+MAX-over-ranks timing and the SUM of the per-type histograms must reproduce a single
+process running all the systems: results do not depend on the GPU count."""
+import json
+import os
+import pathlib
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+ARGS = ["--systems", "2048", "--len", "512", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _line(out):
+    return json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+
+
+def test_two_ranks_match_one_process():
+    env = dict(os.environ)
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                          str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo"] + ARGS,
+                         capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert two.returncode == 0, two.stderr[-3000:]
+    d2 = _line(two.stdout)
+    one = subprocess.run([sys.executable, str(ROOT / "bench.py")] + ARGS[:1] + ["4096"] + ARGS[2:],
+                         capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = _line(one.stdout)
+    assert d2["n_gpus"] == 2 and d2["scaling"] == "weak"
+    assert d2["totals"]["instructions_per_step"] == d1["totals"]["instructions_per_step"] == 4096 * 8 * 512
+    assert d2["totals"]["hist"] == d1["totals"]["hist"]
+    assert d2["totals"]["rounds_total"] == d1["totals"]["rounds_total"]
+    assert d2["totals"]["err_systems"] == d1["totals"]["err_systems"]
+    # value = all ranks' instructions / max-over-ranks time
+    assert abs(d2["value"] - 4096 * 8 * 512 / (d2["ms_per_step"] / 1e3)) < 1e-6 * d2["value"]

@@ -19,9 +19,9 @@ kind, kname, out = sys.argv[1], sys.argv[2], sys.argv[3]
 agg = collections.defaultdict(float)
 dur = {}
 for d in sys.argv[4:]:
-    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+    for f in sorted(glob.glob(f"{d}/**/*.csv", recursive=True)):
         for row in csv.DictReader(open(f)):
-            if kname not in row["Kernel_Name"]:
+            if "Counter_Name" not in row or kname not in row["Kernel_Name"]:
                 continue
             agg[row["Counter_Name"]] += float(row["Counter_Value"])
             dur[row["Counter_Name"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6

@@ -368,3 +368,30 @@ def test_full_size_sampled_parity(dash, kind):
         assert int(dig[s]) == int(ref["digests"][0]), f"system {s} digest"
         assert int(rnd[s]) == int(ref["rounds"][0]), f"system {s} rounds"
         assert int(err[s]) == int(ref["errors"][0]), f"system {s} errors"
+
+
+def test_overflow_hint_reruns_match(dash):
+    """Repeated runs of the same traces start the systems that overflowed the 16-deep
+    rings one tier deeper on a side stream, concurrently with the first tier (which
+    skips them): every result and statistic equals the first run's; new traces drop
+    the hint (results again equal the oracle's)."""
+    N, CS, L, nsys = 8, 4, 1024, 4096
+    with dash.Engine(nsys, num_procs=N, cache_size=CS, max_instr=L) as eng:
+        eng.generate(0x5EED, L, kind=dash.GEN_CONTENTION)
+        runs = []
+        for _ in range(3):
+            st = eng.run()
+            runs.append((st, [x.copy() for x in eng.read_results()]))
+        s1, r1 = runs[0]
+        assert 0 < s1["tier_systems"][1] and s1["tier_systems"][1] * 32 < nsys  # first tier stays 16
+        for st, r in runs[1:]:
+            assert all(np.array_equal(a, b) for a, b in zip(r1, r))
+            for k in ("hist", "instructions", "rounds_total", "rounds_max", "systems", "err_systems",
+                      "dropped", "tier_systems"):
+                assert st[k] == s1[k], k
+        eng.generate(0xBEEF, L, kind=dash.GEN_CONTENTION)
+        st = eng.run()
+        dig, rnd, err = eng.read_results()
+    ref = run_batch(0xBEEF, 0, nsys, num_procs=N, cache_size=CS, length=L, kind=1, threads=8)
+    assert np.array_equal(dig, ref["digests"]) and np.array_equal(rnd, ref["rounds"])
+    assert np.array_equal(err, ref["errors"]) and st["hist"] == ref["hist"].tolist()

@@ -42,6 +42,15 @@ struct dash_ctx {
     uint32_t* d_event_count = nullptr;  // [sys*N+node]
     uint64_t tier_systems[dash::NUM_TIERS] = {};  // systems run per queue-depth tier, last run
     int auto_tier = 0;                         // adaptive first tier
+    // overflow hint: the systems that overflowed the first tier in earlier
+    // runs of the same traces; the next run starts them one tier deeper on a side stream,
+    // concurrently with the first tier, which skips them. Reset whenever traces change.
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    uint32_t* d_hint = nullptr;  // [num_systems] system ids
+    uint8_t* d_skip = nullptr;   // [num_systems] 1 = in the hint
+    uint64_t hint_n = 0;
+    int hint_tier = -1;
     bool loaded = false;
     bool ran = false;
     char msg[256] = {0};
@@ -70,6 +79,14 @@ static uint32_t next_pow2(uint32_t n) {
     return p;
 }
 
+// new traces: the overflow hint no longer applies
+static hipError_t reset_hint(dash_t* h) {
+    if (h->hint_n == 0) return hipSuccess;
+    h->hint_n = 0;
+    h->hint_tier = -1;
+    return hipMemsetAsync(h->d_skip, 0, std::max<uint64_t>(h->cfg.num_systems, 1), h->stream);
+}
+
 extern "C" {
 
 const char* dash_last_error(const dash_t* h) { return h ? h->msg : "null handle"; }
@@ -92,6 +109,12 @@ static void release(dash_t* h) {
     (void)hipFree(h->d_count);
     (void)hipFree(h->d_events);
     (void)hipFree(h->d_event_count);
+    (void)hipFree(h->d_hint);
+    (void)hipFree(h->d_skip);
+    if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    if (h->side) (void)hipStreamDestroy(h->side);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -157,6 +180,12 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     chk(hipMalloc(&h->d_list[0], std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(list)");
     chk(hipMalloc(&h->d_list[1], std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(list)");
     chk(hipMalloc(&h->d_count, 2 * sizeof(uint32_t)), "hipMalloc(count)");
+    chk(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking), "hipStreamCreate(side)");
+    chk(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming), "hipEventCreate");
+    chk(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming), "hipEventCreate");
+    chk(hipMalloc(&h->d_hint, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(hint)");
+    chk(hipMalloc(&h->d_skip, std::max<uint64_t>(nsys, 1)), "hipMalloc(skip)");
+    if (rc == DASH_OK) chk(hipMemset(h->d_skip, 0, std::max<uint64_t>(nsys, 1)), "hipMemset(skip)");
     if (cfg->num_systems > 0xFFFFFFFFull) rc = fail(h, DASH_EINVAL, "more than 2^32 systems");
     if (cfg->trace_events) {
         if ((double)nsys * N * cfg->trace_events * 8.0 > 64.0 * (1ull << 30))
@@ -207,6 +236,7 @@ int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const u
         HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 8, hipMemcpyHostToDevice, h->stream));
     if (num_systems)
         HIPCHK(h, hipMemcpyAsync(h->d_lens, lens, num_systems * N * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, reset_hint(h));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->loaded = true;
     h->ran = false;
@@ -232,6 +262,7 @@ int dash_generate(dash_t* h, const dash_gen* g) {
     a.len = g->len;
     HIPCHK(h, hipSetDevice(h->cfg.device));
     HIPCHK(h, dash::launch_gen(a, h->stream));
+    HIPCHK(h, reset_hint(h));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->loaded = true;
     h->ran = false;
@@ -272,27 +303,63 @@ int dash_run(dash_t* h, dash_stats* stats) {
     const uint32_t* list = nullptr;
     const uint32_t f = h->cfg.flags;
     const int first = (f & DASH_TIER_FROM_256) ? 2 : (f & DASH_TIER_FROM_32) ? 1 : h->auto_tier;
+    if (h->hint_n && h->hint_tier != first) HIPCHK(h, reset_hint(h));
+    // Systems that overflowed the first tier in an earlier run of these traces (the
+    // schedule is deterministic, so they will again) start one tier deeper on the side
+    // stream right away, while the first tier -- which skips them -- runs on the main
+    // stream: the deeper pass no longer waits for the first tier's tail.
+    const bool hint = h->hint_n > 0 && first < dash::NUM_TIERS - 1;
+    const int ht = first + 1;
+    if (hint) {
+        HIPCHK(h, hipMemsetAsync(h->d_count + (ht & 1), 0, sizeof(uint32_t), h->stream));
+        HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+        HIPCHK(h, hipStreamWaitEvent(h->side, h->ev_fork, 0));
+        dash::SimArgs b = a;
+        b.sys_list = h->d_hint;
+        b.list_len = h->hint_n;
+        b.final_tier = ht == dash::NUM_TIERS - 1 ? 1u : 0u;
+        b.ovf_list = h->d_list[ht & 1];  // shared with the main stream's pass at this tier
+        b.ovf_count = h->d_count + (ht & 1);
+        HIPCHK(h, dash::launch_sim(b, h->seg, h->cfg.cache_size, dash::RING_TIERS[ht],
+                                   (h->hint_n + spw - 1) / spw, h->side));
+        HIPCHK(h, hipEventRecord(h->ev_join, h->side));
+    }
+    uint64_t first_ovf = 0;  // systems that overflowed the first tier in this run
     for (int tier = 0; tier < dash::NUM_TIERS; ++tier) h->tier_systems[tier] = 0;
     for (int tier = first; tier < dash::NUM_TIERS; ++tier) {
         const bool last = tier == dash::NUM_TIERS - 1;
-        h->tier_systems[tier] = todo;
-        if (todo == 0) continue;
+        const bool joined = hint && tier == ht;  // the hinted pass ran this tier too
+        h->tier_systems[tier] = todo + (joined ? h->hint_n : 0);
         uint32_t* out = h->d_list[tier & 1];
         uint32_t* cnt = h->d_count + (tier & 1);
-        a.sys_list = list;
-        a.list_len = todo;
-        a.final_tier = last ? 1u : 0u;
-        a.ovf_list = out;
-        a.ovf_count = cnt;
-        HIPCHK(h, hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
-        HIPCHK(h, dash::launch_sim(a, h->seg, h->cfg.cache_size, dash::RING_TIERS[tier], (todo + spw - 1) / spw,
-                                   h->stream));
+        if (!joined) HIPCHK(h, hipMemsetAsync(cnt, 0, sizeof(uint32_t), h->stream));
+        if (todo) {
+            a.sys_list = list;
+            a.list_len = todo;
+            a.final_tier = last ? 1u : 0u;
+            a.ovf_list = out;
+            a.ovf_count = cnt;
+            a.skip = (hint && tier == first) ? h->d_skip : nullptr;
+            HIPCHK(h, dash::launch_sim(a, h->seg, h->cfg.cache_size, dash::RING_TIERS[tier],
+                                       (todo + spw - 1) / spw, h->stream));
+        }
+        if (joined) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_join, 0));
         if (last) break;
         uint32_t next = 0;
-        HIPCHK(h, hipMemcpyAsync(&next, cnt, sizeof next, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (todo || joined) {
+            HIPCHK(h, hipMemcpyAsync(&next, cnt, sizeof next, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
+        if (tier == first) first_ovf = next;
         todo = next;
         list = out;
+    }
+    if (first < dash::NUM_TIERS - 1 && first_ovf) {  // they join the hint for the next run
+        HIPCHK(h, hipMemcpyAsync(h->d_hint + h->hint_n, h->d_list[first & 1], first_ovf * sizeof(uint32_t),
+                                 hipMemcpyDeviceToDevice, h->stream));
+        HIPCHK(h, dash::launch_mark(h->d_list[first & 1], first_ovf, h->d_skip, h->stream));
+        h->hint_n += first_ovf;
+        h->hint_tier = first;
     }
     if (!(f & (DASH_TIER_FROM_32 | DASH_TIER_FROM_256)) && first < dash::NUM_TIERS - 1 &&
         h->tier_systems[first + 1] * 32 > h->tier_systems[first])

@@ -50,6 +50,7 @@ struct SimArgs {
     uint32_t* event_count;    // [sys*N+node] events produced (may exceed event_cap)
     unsigned long long* stats;  // [STAT_WORDS]
     uint64_t arb_seed;        // 0: lowest-sender-first lockstep; else the seeded schedule
+    const uint8_t* skip;      // optional [sys]: 1 = run elsewhere this pass (a deeper tier, concurrently)
 };
 
 struct GenArgs {
@@ -76,5 +77,7 @@ constexpr int NUM_TIERS = 3;
 constexpr uint32_t RING_TIERS[NUM_TIERS] = {16, 32, 256};
 constexpr uint32_t CHUNK_INSTR = 4;  // instructions per 8-B trace chunk
 hipError_t launch_gen(const GenArgs& g, hipStream_t s);
+// skip[list[i]] = 1 for i < n
+hipError_t launch_mark(const uint32_t* list, uint64_t n, uint8_t* skip, hipStream_t s);
 
 }  // namespace dash

@@ -129,7 +129,8 @@ void sim_kernel(const SimArgs a) {
         live = slot_id < a.list_len && t < N;
         sys = slot_id < a.list_len ? a.sys_list[slot_id] : 0;
     } else {
-        live = slot_id < a.nsys && t < N;
+        // a system the host already runs at a deeper tier (its overflow hint) sits out
+        live = slot_id < a.nsys && t < N && !(a.skip && a.skip[slot_id]);
         sys = slot_id;
     }
     uint32_t len = live ? a.lens[sys * N + t] : 0u;
@@ -659,6 +660,18 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring
     case 8: return launch_sim_p<8>(a, cs, ring, groups, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+__global__ __launch_bounds__(256) void mark_kernel(const uint32_t* list, uint64_t n, uint8_t* skip) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        skip[list[i]] = 1;
+}
+
+hipError_t launch_mark(const uint32_t* list, uint64_t n, uint8_t* skip, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(mark_kernel, dim3(blocks), dim3(256), 0, s, list, n, skip);
+    return hipGetLastError();
 }
 
 hipError_t launch_gen(const GenArgs& g, hipStream_t s) {

@@ -112,7 +112,7 @@ def test_cli_reference_argv_contract(dash, tmp_path):
 
 
 @pytest.mark.parametrize("N,CS", [(4, 4), (8, 4), (4, 1), (8, 2), (8, 8), (8, 16), (2, 4),
-                                  (3, 4), (5, 2), (1, 4)])
+                                  (3, 4), (5, 2), (1, 4), (6, 4), (7, 8), (8, 1), (4, 16)])
 def test_random_traces_bit_exact(dash, N, CS):
     rng = np.random.default_rng(1000 * N + CS)
     packed, lens = random_batch(rng, 160, N, 40)

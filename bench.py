@@ -265,6 +265,9 @@ def main():
                             "frac_of_simd32_issue": prof["valu_per_launch"] / (prof["kernel_ms"] / 1e3)
                             / VALU_PEAK_SIMD32,
                             "valu_per_wave_round": prof["valu_per_launch"] / max(stats["wave_rounds"], 1),
+                            "salu_per_wave_round": prof.get("sq_insts_salu", 0.0) / max(stats["wave_rounds"], 1),
+                            "lds_bank_conflict_frac": (prof["sq_lds_bank_conflict"] / prof["sq_lds_idx_active"]
+                                                       if prof.get("sq_lds_idx_active") else None),
                             "l2_hit_rate": prof.get("l2_hit_rate"),
                             "source": prof.get("source")} if prof else None),
             "cpu_baseline": cpu,

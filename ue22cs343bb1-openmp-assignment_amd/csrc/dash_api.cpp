@@ -132,6 +132,9 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     if (N < 1 || N > DASH_MAX_PROCS) return DASH_EINVAL;
     if (CS < 1 || CS > DASH_MAX_CACHE || (CS & (CS - 1))) return DASH_EINVAL;
     if (cfg->max_instr > (1u << 24)) return DASH_EINVAL;
+    if (cfg->num_systems > 0xFFFFFFFFull) return DASH_EINVAL;  // system ids are u32 in the lists
+    if (cfg->trace_events && (double)cfg->num_systems * N * cfg->trace_events * 8.0 > 64.0 * (1ull << 30))
+        return DASH_EINVAL;  // event log larger than 64 GiB
     dash_t* h = new (std::nothrow) dash_ctx();
     if (!h) return DASH_ENOMEM;
     h->cfg = *cfg;
@@ -186,10 +189,7 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     chk(hipMalloc(&h->d_hint, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(hint)");
     chk(hipMalloc(&h->d_skip, std::max<uint64_t>(nsys, 1)), "hipMalloc(skip)");
     if (rc == DASH_OK) chk(hipMemset(h->d_skip, 0, std::max<uint64_t>(nsys, 1)), "hipMemset(skip)");
-    if (cfg->num_systems > 0xFFFFFFFFull) rc = fail(h, DASH_EINVAL, "more than 2^32 systems");
     if (cfg->trace_events) {
-        if ((double)nsys * N * cfg->trace_events * 8.0 > 64.0 * (1ull << 30))
-            rc = fail(h, DASH_EINVAL, "event log larger than 64 GiB");
         chk(hipMalloc(&h->d_events, std::max<uint64_t>(nsys * N * cfg->trace_events, 1) * 8), "hipMalloc(events)");
         chk(hipMalloc(&h->d_event_count, std::max<uint64_t>(nsys * N, 1) * 4), "hipMalloc(event_count)");
     }

@@ -75,7 +75,7 @@ enum dash_txn {
 
 typedef struct dash_cfg {
     uint32_t num_procs;   /* NUM_PROCS (ref :6): 4 or 8 */
-    uint32_t cache_size;  /* CACHE_SIZE (ref :7): 1, 2, 4, 8 or 16 */
+    uint32_t cache_size;  /* CACHE_SIZE (ref :7): 1..16 (powers of two have specialised kernels) */
     uint32_t max_instr;   /* longest trace per node (ref MAX_INSTR_NUM 32, :10) */
     uint32_t flags;       /* DASH_KEEP_STATE */
     uint64_t num_systems; /* independent systems in the batch */

@@ -426,7 +426,7 @@ uint64_t orc_digest_node(const orc_node_state *s, int node_id, int cache_size) {
 int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
                    const uint32_t *lens, orc_result *out, char *log, uint64_t log_cap) {
     const int N = cfg->num_procs, CS = cfg->cache_size;
-    if (N < 1 || N > ORC_MAX_PROCS || CS < 1 || CS > ORC_MAX_CACHE || (CS & (CS - 1)) ||
+    if (N < 1 || N > ORC_MAX_PROCS || CS < 1 || CS > ORC_MAX_CACHE ||
         cfg->ring_depth < 1 || cfg->ring_depth > MAX_RING)
         return -1;
     for (int t = 0; t < N; t++)
@@ -815,7 +815,7 @@ static int x_setup(xctx *c, const orc_cfg *cfg, const uint16_t *trace, uint64_t 
     memset(c, 0, sizeof *c);
     c->N = cfg->num_procs;
     c->CS = cfg->cache_size;
-    if (c->N < 1 || c->N > ORC_MAX_PROCS || c->CS < 1 || c->CS > ORC_MAX_CACHE || (c->CS & (c->CS - 1))) return -1;
+    if (c->N < 1 || c->N > ORC_MAX_PROCS || c->CS < 1 || c->CS > ORC_MAX_CACHE) return -1;
     for (int t = 0; t < c->N; t++) {
         c->trace[t] = trace + (uint64_t)t * stride;
         c->count[t] = lens[t];

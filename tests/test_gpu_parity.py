@@ -395,3 +395,15 @@ def test_overflow_hint_reruns_match(dash):
     ref = run_batch(0xBEEF, 0, nsys, num_procs=N, cache_size=CS, length=L, kind=1, threads=8)
     assert np.array_equal(dig, ref["digests"]) and np.array_equal(rnd, ref["rounds"])
     assert np.array_equal(err, ref["errors"]) and st["hist"] == ref["hist"].tolist()
+
+
+@pytest.mark.parametrize("N,CS", [(8, 3), (4, 5), (8, 6), (8, 7), (5, 12), (8, 15)])
+def test_non_power_of_two_cache_size(dash, N, CS):
+    """CACHE_SIZE is a free #define in the reference (cacheIndex = blockIndex % CACHE_SIZE,
+    ref :188): non-powers of two run on the generic kernel (runtime modulo, LDS sized for
+    16 lines) and match the oracle bit-exactly, including dumps."""
+    rng = np.random.default_rng(4000 + 16 * N + CS)
+    packed, lens = random_batch(rng, 96, N, 40)
+    check_batch(dash, packed, lens, N, CS)
+    packed, lens = random_batch(rng, 48, N, 48, block_span=6, hot_frac=0.4)
+    check_batch(dash, packed, lens, N, CS)

@@ -130,7 +130,7 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     *out = nullptr;
     const uint32_t N = cfg->num_procs, CS = cfg->cache_size;
     if (N < 1 || N > DASH_MAX_PROCS) return DASH_EINVAL;
-    if (CS < 1 || CS > DASH_MAX_CACHE || (CS & (CS - 1))) return DASH_EINVAL;
+    if (CS < 1 || CS > DASH_MAX_CACHE) return DASH_EINVAL;  // any CACHE_SIZE 1..16 (ref :7)
     if (cfg->max_instr > (1u << 24)) return DASH_EINVAL;
     if (cfg->num_systems > 0xFFFFFFFFull) return DASH_EINVAL;  // system ids are u32 in the lists
     if (cfg->trace_events && (double)cfg->num_systems * N * cfg->trace_events * 8.0 > 64.0 * (1ull << 30))
@@ -287,6 +287,9 @@ int dash_run(dash_t* h, dash_stats* stats) {
     a.keep = (h->cfg.flags & DASH_KEEP_STATE) ? 1u : 0u;
     a.event_cap = h->cfg.trace_events;
     a.arb_seed = h->cfg.schedule_seed;
+    a.cache_size = h->cfg.cache_size;
+    for (uint32_t b = 0; b < 16; b++)  // b % CACHE_SIZE for the generic (non-power-of-two) kernels
+        a.cs_lut |= (uint64_t)(b % h->cfg.cache_size) << (4 * b);
     a.events = h->d_events;
     a.event_count = h->d_event_count;
     a.stats = h->d_stats;

@@ -51,6 +51,8 @@ struct SimArgs {
     unsigned long long* stats;  // [STAT_WORDS]
     uint64_t arb_seed;        // 0: lowest-sender-first lockstep; else the seeded schedule
     const uint8_t* skip;      // optional [sys]: 1 = run elsewhere this pass (a deeper tier, concurrently)
+    uint32_t cache_size;      // CACHE_SIZE (ref :7); read by the generic (non-power-of-two) kernels
+    uint64_t cs_lut;          // nibble b = b % cache_size, b < 16 (generic kernels)
 };
 
 struct GenArgs {

@@ -78,11 +78,16 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
     return k;
 }
 
+// CS = CACHE_SIZE; CS = 0 is the generic kernel for a non-power-of-two CACHE_SIZE (read at
+// run time, LDS sized for the maximum of 16 lines)
+template <int CS>
+constexpr int cs_rows() { return CS ? CS : 16; }
+
 template <int P, int CS, uint32_t RING>
 struct Lds {  // 32-bit word offsets
     static constexpr uint32_t ENT = 0;                      // u16 [16][64]  mem | bitVector<<8   (swizzled)
     static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8      (swizzled)
-    static constexpr uint32_t RNG = CAC + CS * 64 / 2;      // u32 [RING][64] message words
+    static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
     static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
     static constexpr uint32_t HST = WND + WIN * WCHUNK * 64 / 2;  // u32 [13][64/P+1] per-system counters
@@ -109,6 +114,7 @@ __attribute__((amdgpu_waves_per_eu(DASH_WAVES_PER_EU)))
 #endif
 void sim_kernel(const SimArgs a) {
     using L = Lds<P, CS, RING>;
+    const uint32_t ncs = CS ? (uint32_t)CS : a.cache_size;  // cache lines per node
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
     __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS];
@@ -141,7 +147,7 @@ void sim_kernel(const SimArgs a) {
 #pragma unroll
     for (uint32_t b = 0; b < 16; ++b) lds16[L::ENT * 2 + b * 64 + sw] = (uint16_t)((20u * t + b) & 0xFFu);
 #pragma unroll
-    for (uint32_t i = 0; i < CS; ++i) lds16[L::CAC * 2 + i * 64 + sw] = 0xFFu;
+    for (uint32_t i = 0; i < ncs; ++i) lds16[L::CAC * 2 + i * 64 + sw] = 0xFFu;
     for (uint32_t w = lane; w < 13 * L::HSTRIDE; w += 64) lds[L::HST + w] = 0u;
     lds[L::MQ + 2 * lane] = 0u;
     char* const ldsb = reinterpret_cast<char*>(lds);
@@ -276,7 +282,8 @@ void sim_kernel(const SimArgs a) {
         const uint32_t addr = (mw >> 8) & 0x7Fu;
         const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
-        const uint32_t idx = b & (CS - 1);
+        // cacheIndex = blockIndex % CACHE_SIZE (ref :188)
+        const uint32_t idx = CS ? b % (uint32_t)CS : (uint32_t)(a.cs_lut >> (4 * b)) & 15u;
         uint16_t* const ent = lds16 + L::ENT * 2 + b * 64 + sw;
         uint16_t* const cac = lds16 + L::CAC * 2 + idx * 64 + sw;
         const uint32_t e16 = *ent;
@@ -490,7 +497,7 @@ void sim_kernel(const SimArgs a) {
     uint64_t h = 0x243F6A8885A308D3ull ^ ((uint64_t)t << 56);
     for (uint32_t b = 0; b < 16; ++b)
         h = fmix64(h ^ (uint64_t)(lds16[L::ENT * 2 + b * 64 + sw] | (((dsv >> (2 * b)) & 3u) << 16)));
-    for (uint32_t i = 0; i < CS; ++i)
+    for (uint32_t i = 0; i < ncs; ++i)
         h = fmix64(h ^ ((uint64_t)(lds16[L::CAC * 2 + i * 64 + sw] | (((cst >> (2 * i)) & 3u) << 16)) |
                         (1ull << 24)));
     uint64_t dg = 0x9E3779B97F4A7C15ull;
@@ -508,10 +515,10 @@ void sim_kernel(const SimArgs a) {
     if (a.events && report) a.event_count[sys * N + t] = nev;
     maxd >>= 8;  // ring-slot bytes -> messages
     if (a.state && report) {
-        uint32_t* st = a.state + (sys * N + t) * (16 + CS);
+        uint32_t* st = a.state + (sys * N + t) * (16 + ncs);
         for (uint32_t b = 0; b < 16; ++b)
             st[b] = lds16[L::ENT * 2 + b * 64 + sw] | (((dsv >> (2 * b)) & 3u) << 16);
-        for (uint32_t i = 0; i < CS; ++i)
+        for (uint32_t i = 0; i < ncs; ++i)
             st[16 + i] = lds16[L::CAC * 2 + i * 64 + sw] | (((cst >> (2 * i)) & 3u) << 16);
     }
     if (report && t == 0 && a.keep)
@@ -646,7 +653,7 @@ static hipError_t launch_sim_p(const SimArgs& a, uint32_t cs, uint32_t ring, uin
     case 4: return launch_sim_pc<P, 4>(a, ring, groups, s);
     case 8: return launch_sim_pc<P, 8>(a, ring, groups, s);
     case 16: return launch_sim_pc<P, 16>(a, ring, groups, s);
-    default: return hipErrorInvalidValue;
+    default: return cs >= 1 && cs <= 16 ? launch_sim_pc<P, 0>(a, ring, groups, s) : hipErrorInvalidValue;
     }
 }
 

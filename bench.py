@@ -272,6 +272,7 @@ def main():
                             "source": prof.get("source")} if prof else None),
             "cpu_baseline": cpu,
             "kernel_ms_avg": avg_kernel_s * 1e3,
+            "kernel_ms_steps": [round(x, 3) for x in kernel_ms],
             "tier_systems": stats["tier_systems"],
             "wave_rounds": stats["wave_rounds"],
             "totals": {"hist": totals[:13], "instructions_per_step": totals[13],

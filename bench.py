@@ -62,6 +62,66 @@ def cpu_baseline(args, seed, kind, locality, target_s):
                       f"oracle/dash_oracle.c lockstep restatement of assignment.c"}
 
 
+def ref_baseline(args, seed, kind_id, target_s):
+    """The reference itself (oracle/_ref/cache_simulator_bench: assignment.c with the
+    benchmark patch of SURVEY.md §8(d), gcc -O2 -fopenmp, 8 spinning OpenMP threads per
+    instance) on systems 0.. of the same synthetic workload, written as the reference's
+    tests/<dir>/core_<n>.txt. `--ref-instances` processes run concurrently (the north
+    star's "as many concurrent instances as host cores"; 1 = one 8-thread instance);
+    batches repeat until `target_s` has passed."""
+    import subprocess
+    import tempfile
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ctypes as oc
+    exe = ROOT / "oracle" / "_ref" / "cache_simulator_bench"
+    if not exe.exists():
+        raise SystemExit(f"{exe} missing: build it with oracle/build_ref.sh where /root/reference exists")
+    k = args.ref_instances
+    with tempfile.TemporaryDirectory() as td:
+        dirs = []
+        for i in range(k):
+            d = pathlib.Path(td, f"i{i}")
+            (d / "tests" / "b").mkdir(parents=True)
+            tr = oc.gen_system(seed, i, num_procs=8, length=args.len, kind=kind_id)
+            for n in range(8):
+                lines = []
+                for w in tr[n].tolist():
+                    a, v = (w >> 8) & 0x7F, w & 0xFF
+                    lines.append(f"WR {a:02X} {v}\n" if w & 0x8000 else f"RD {a:02X}\n")
+                (d / "tests" / "b" / f"core_{n}.txt").write_text("".join(lines))
+            dirs.append(d)
+        batches, t0 = 0, time.perf_counter()
+        while True:
+            procs = [subprocess.Popen([str(exe), "b"], cwd=d, stdout=subprocess.DEVNULL) for d in dirs]
+            tb, last = time.perf_counter(), time.perf_counter()
+            while any(p.poll() is None for p in procs):  # spinning instances can take minutes
+                time.sleep(0.02)
+                now = time.perf_counter()
+                if now - tb > 900:
+                    for p in procs:
+                        p.kill()
+                    raise SystemExit("reference instances did not finish within 900 s")
+                if now - last > 30:
+                    last = now
+                    print(f"[ref_baseline] {sum(p.poll() is not None for p in procs)}/{k} instances done, "
+                          f"{now - tb:.0f} s", file=sys.stderr, flush=True)
+            if any(p.returncode != 0 for p in procs):
+                raise SystemExit(f"reference instance exited with {[p.returncode for p in procs]}")
+            batches += 1
+            elapsed = time.perf_counter() - t0
+            if elapsed >= target_s:
+                break
+        for d in dirs:  # every instance reached quiescence and dumped its 8 nodes
+            assert all((d / f"core_{n}_output.txt").exists() for n in range(8)), d
+    instr = batches * k * 8 * args.len
+    cores = min(len(os.sched_getaffinity(0)), args.cpu_threads)
+    return {"value": instr / elapsed, "unit": "instr/s", "cores": cores, "kind": "reference",
+            "sample": f"{batches} batch(es) x {k} concurrent instance(s) x 8 OpenMP threads, one 8-node system "
+                      f"x {args.len} instr each ({args.kind}, CS=4, systems 0..{k - 1} of seed 0x{seed:X}) "
+                      f"in {elapsed:.1f} s; assignment.c + benchmark patch (oracle/patch_ref.py), "
+                      f"gcc -O2 -fopenmp"}
+
+
 def shard(rank, world, per_gpu):
     """Weak scaling: rank g owns global systems [g*M, (g+1)*M). Traces are keyed
     by global id, so results do not depend on the GPU count."""
@@ -164,6 +224,11 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-kind", choices=["port", "reference"], default="port",
+                    help="cpu_baseline leg: the oracle port on --cpu-threads threads, or the reference "
+                         "binary itself (oracle/_ref/cache_simulator_bench)")
+    ap.add_argument("--ref-instances", type=int, default=1,
+                    help="concurrent reference instances for --cpu-kind reference")
     ap.add_argument("--first-depth", type=int, choices=[0, 32, 256], default=0,
                     help="first queue-depth tier (0 = adaptive, starting at 16)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -234,7 +299,12 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args, args.seed, kind, locality, args.cpu_seconds)
+            if args.cpu_kind == "reference":
+                if args.cache_size != 4 or args.kind == "locality":
+                    raise SystemExit("the reference baseline binary is built for CACHE_SIZE 4, uniform/contention")
+                cpu = ref_baseline(args, args.seed, kind, args.cpu_seconds)
+            else:
+                cpu = cpu_baseline(args, args.seed, kind, locality, args.cpu_seconds)
         line = {
             "metric": "simulated instr/sec (whole node), 8-core DASH systems; % HBM roofline",
             "value": value,

@@ -14,3 +14,7 @@ fi
 mkdir -p "$OUT"
 gcc -O0 -fopenmp -w -o "$OUT/cache_simulator" "$REF/assignment.c"
 echo "built $OUT/cache_simulator"
+# oracle/_ref/cache_simulator_bench: the reference with the benchmark patch of
+# SURVEY.md §8(d) (atomic queue counts, receiver guard, termination), 8 nodes,
+# 4096 instructions, gcc -O2 -fopenmp -- the CPU baseline bench.py can time
+python3 "$(dirname "$0")/patch_ref.py" "$REF"

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""TEST INFRASTRUCTURE: build the reference simulator as a benchmark binary.
+
+Reads /root/reference/assignment.c where it lies, applies the minimal patch of
+SURVEY.md §8(d) / BASELINE.md to a copy in a temporary directory (never inside
+this repository), and compiles it with `gcc -O2 -fopenmp` into
+oracle/_ref/cache_simulator_bench (git-ignored; it travels to the GPU box like
+the other built files). Only bench.py's cpu_baseline leg runs it.
+
+The patch (each edit is anchored on text that must occur exactly once):
+  1. NUM_PROCS, CACHE_SIZE, MAX_INSTR_NUM become -D overridable (ref :6-10);
+  2. the queue count is atomic on both sides -- dequeue `count--` (ref :177) and
+     enqueue `count++` (ref :757) -- and the consumer's `count > 0` test is an
+     atomic load (ref :169); without this, 4096-instruction runs hang;
+  3. sendMessage drops a message to a receiver >= NUM_PROCS (ref :751; the
+     0xFF-line eviction of ref :772,786 would index messageBuffers[15]);
+  4. termination: a global in-flight counter (incremented on every successful
+     enqueue, decremented after a message's handler finishes, ref :619) and a
+     count of threads whose instructions are all done; a thread that has printed
+     its final state (ref :632-646) exits once every thread is done and nothing
+     is in flight. The unpatched program never exits (ref :165).
+Everything else -- the handlers, locks, spinning, state dumps -- is the reference.
+"""
+import pathlib
+import subprocess
+import sys
+import tempfile
+
+EDITS = [
+    ("#define NUM_PROCS 4\n", "#ifndef NUM_PROCS\n#define NUM_PROCS 4\n#endif\n"),
+    ("#define CACHE_SIZE 4\n", "#ifndef CACHE_SIZE\n#define CACHE_SIZE 4\n#endif\n"),
+    ("#define MAX_INSTR_NUM 32\n", "#ifndef MAX_INSTR_NUM\n#define MAX_INSTR_NUM 32\n#endif\n"),
+    ("omp_lock_t msgBufferLocks[ NUM_PROCS ];\n",
+     "omp_lock_t msgBufferLocks[ NUM_PROCS ];\n"
+     "static long bench_inflight = 0;  /* patch 4 */\n"
+     "static int bench_done = 0;\n"),
+    ("                messageBuffers[ threadId ].count > 0 &&",
+     "                __atomic_load_n( &messageBuffers[ threadId ].count, __ATOMIC_SEQ_CST ) > 0 &&"),
+    ("                messageBuffers[ threadId ].count--;\n",
+     "                __atomic_fetch_sub( &messageBuffers[ threadId ].count, 1, __ATOMIC_SEQ_CST );\n"),
+    ("                        break;\n                }\n            }\n            \n"
+     "            // Check if we are waiting for a reply message",
+     "                        break;\n                }\n"
+     "                __atomic_fetch_sub( &bench_inflight, 1, __ATOMIC_SEQ_CST );\n"
+     "            }\n            \n            // Check if we are waiting for a reply message"),
+    ("        byte waitingForReply = 0;",
+     "        int benchFinished = 0;\n        byte waitingForReply = 0;"),
+    ("                    printProcessorState( threadId, node );\n                    printProcState--;\n"
+     "                }\n",
+     "                    printProcessorState( threadId, node );\n                    printProcState--;\n"
+     "                }\n"
+     "                if ( !benchFinished ) {\n"
+     "                    benchFinished = 1;\n"
+     "                    __atomic_fetch_add( &bench_done, 1, __ATOMIC_SEQ_CST );\n"
+     "                }\n"
+     "                if ( __atomic_load_n( &bench_done, __ATOMIC_SEQ_CST ) == NUM_PROCS &&\n"
+     "                     __atomic_load_n( &bench_inflight, __ATOMIC_SEQ_CST ) == 0 )\n"
+     "                    break;\n"),
+    ("    omp_set_lock( &msgBufferLocks[ receiver ] );\n",
+     "    if ( receiver < 0 || receiver >= NUM_PROCS ) return;  /* patch 3 */\n"
+     "    omp_set_lock( &msgBufferLocks[ receiver ] );\n"),
+    ("      buf->count++;\n",
+     "      __atomic_fetch_add( &bench_inflight, 1, __ATOMIC_SEQ_CST );\n"
+     "      __atomic_fetch_add( &buf->count, 1, __ATOMIC_SEQ_CST );\n"),
+]
+
+
+def main():
+    ref = pathlib.Path(sys.argv[1] if len(sys.argv) > 1 else "/root/reference") / "assignment.c"
+    out = pathlib.Path(__file__).resolve().parent / "_ref" / "cache_simulator_bench"
+    if not ref.exists():
+        print(f"reference not present at {ref}; skipping", file=sys.stderr)
+        return 0
+    src = ref.read_text()
+    for old, new in EDITS:
+        n = src.count(old)
+        if n != 1:
+            raise SystemExit(f"patch anchor found {n} times: {old[:60]!r}")
+        src = src.replace(old, new)
+    out.parent.mkdir(parents=True, exist_ok=True)
+    with tempfile.TemporaryDirectory() as td:
+        c = pathlib.Path(td) / "assignment_bench.c"
+        c.write_text(src)
+        subprocess.run(["gcc", "-O2", "-fopenmp", "-w", "-DNUM_PROCS=8", "-DMAX_INSTR_NUM=4096",
+                        "-DCACHE_SIZE=4", "-o", str(out), str(c)], check=True)
+    print(f"built {out}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -51,3 +51,33 @@ def test_self_home_traces_match_reference_binary(tmp_path, seed):
                      ring_depth=256)
     for n in range(4):
         assert (tmp_path / f"core_{n}_output.txt").read_text() == dump_node(res, n, 4), f"node {n}"
+
+
+BENCH = ROOT / "oracle" / "_ref" / "cache_simulator_bench"
+
+
+@pytest.mark.skipif(not BENCH.exists(), reason="benchmark reference binary not built")
+@pytest.mark.parametrize("seed", range(4))
+def test_benchmark_build_of_reference_matches_oracle(tmp_path, seed):
+    """oracle/_ref/cache_simulator_bench (the reference + the benchmark patch of
+    oracle/patch_ref.py: 8 nodes, 4096 instructions, atomic counts, termination) is
+    bench.py's `--cpu-kind reference` baseline. On self-homed 8-node traces of up to 4096
+    instructions it must terminate by itself and dump exactly the oracle's final state."""
+    rng = np.random.default_rng(100 + seed)
+    rows = []
+    for n in range(8):
+        k = int(rng.integers(1, 4097))
+        ws = rng.random(k) < 0.5
+        rows.append([pack("W" if w else "R", (n << 4) | int(b), int(v) if w else 0)
+                     for w, b, v in zip(ws, rng.integers(0, 16, k), rng.integers(0, 256, k))])
+    write_trace(tmp_path / "tests" / "t", rows)
+    p = subprocess.run(["timeout", "60", str(BENCH), "t"], cwd=tmp_path, capture_output=True)
+    assert p.returncode == 0, p.stderr  # exits on its own (patch 4)
+    L = max(len(r) for r in rows)
+    tr = np.zeros((8, L), np.uint16)
+    for n, r in enumerate(rows):
+        tr[n, :len(r)] = r
+    res = run_system(tr, np.array([len(r) for r in rows], np.uint32), num_procs=8, cache_size=4,
+                     ring_depth=256)
+    for n in range(8):
+        assert (tmp_path / f"core_{n}_output.txt").read_text() == dump_node(res, n, 4), f"node {n}"

@@ -10,9 +10,10 @@
 //     workgroup's LDS ([slot][lane] arrays: every per-lane access is bank-conflict
 //     free) or in lane registers;
 //   * lockstep rounds: each lane pops one message or issues one instruction,
-//     then all sends of the round are delivered with a segmented prefix sum
-//     over the P lanes (lowest sender first, program order inside a sender)
-//     straight into the receivers' LDS rings -- no locks, no atomics;
+//     then all sends of the round are delivered straight into the receivers'
+//     LDS rings, lowest sender first and in program order inside a sender:
+//     senders OR a bit into the receiver's LDS arrival mask and take the slot
+//     `tail + (arrival bits below their own)` -- no locks, no scans;
 //   * queue depth is tiered: a pass with RING-deep queues halts and lists any
 //     system that would overflow; the listed systems are re-simulated from
 //     scratch with deeper queues, the last tier being the reference's 256

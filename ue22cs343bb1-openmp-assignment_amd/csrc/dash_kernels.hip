@@ -53,7 +53,7 @@ constexpr uint32_t WCHUNK = DASH_WCHUNK;  // instructions per window refill (2: 
 static_assert(WCHUNK == 2 || WCHUNK == 4, "window chunk");
 using wchunk_t = typename std::conditional<WCHUNK == 4, uint2, uint32_t>::type;
 #ifndef DASH_QCHECK
-#define DASH_QCHECK 4              // rounds between quiescence votes (a multiple of WCHUNK)
+#define DASH_QCHECK 4              // rounds between quiescence votes (= WCHUNK: one trip of the round loop)
 #endif
 #ifndef DASH_MASKED_STORE
 #define DASH_MASKED_STORE 0
@@ -186,8 +186,11 @@ void sim_kernel(const SimArgs a) {
     // its LDS ring in ring-slot bytes (x SLOT), owned by the node; senders learn
     // them through MQ each round. Below the final depth the count is not clamped:
     // exceeding RING is the overflow that hands the system to the next depth.
-    uint32_t cq = 0, tq = 0;
-    uint32_t pc = 0, last_val = 0;
+    uint32_t cq = 0, tq = lane * 4u;  // tail carries this node's ring column (bits below the slot)
+    // program counter and trace length pre-scaled by the window row stride (128 B), so
+    // the window address of the next instruction is one and-or
+    constexpr uint32_t PCU = 128;
+    uint32_t pc = 0, last_val = 0, lenx = len * PCU;
     // waitingForReply (ref :157) of every lane as one wave mask: updated by the scalar
     // unit, read per lane through inverse_ballot (no VALU)
     uint64_t wmask = 0;
@@ -197,18 +200,21 @@ void sim_kernel(const SimArgs a) {
     const uint32_t cap = a.max_rounds;
 
     const uint32_t wES = T_ES | (t << 4), wEM = T_EMOD | (t << 4);  // eviction notice, sender part
-    // the queue tail a node publishes carries its own ring column (lane * 4 B) in
-    // the bits below the slot: a sender's slot address is tail + rank slots, masked
-    const uint32_t col = lane * 4u;
 
     uint32_t r = 0;
-    for (;; ++r) {
+    // WCHUNK rounds per trip, unrolled: the housekeeping point (refill, quiescence vote,
+    // overflow stop) is the first round of every trip, a compile-time position
+    static_assert(DASH_QCHECK == WCHUNK, "one housekeeping point per WCHUNK rounds");
+    for (bool done = false; !done;)
+#pragma unroll
+    for (uint32_t k = 0; k < WCHUNK; ++k, ++r) {
         // ---- quiescence / round cap, on start-of-round state ----
         // A system is active while any of its nodes has a message or can issue;
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
         const bool waiting = __builtin_amdgcn_inverse_ballot_w64(wmask);
-        bool can_issue = !waiting & (pc < len);
-        bool active = (cq != 0) | can_issue;
+        bool can_issue = !waiting & (pc < lenx);
+        bool nonempty = cq != 0;
+        bool active = nonempty | can_issue;
         if (r == cap) {  // wave-uniform: every system still active has run `cap` rounds
             COLD();
             const uint64_t act = vote(active);
@@ -216,8 +222,9 @@ void sim_kernel(const SimArgs a) {
             wmask &= ~vote(kill);
             if (kill) {
                 err |= DASH_ERR_ROUNDCAP_D;
+                nonempty = false;
                 cq = 0;
-                len = pc;
+                lenx = pc;
                 can_issue = false;
                 active = false;
             }
@@ -232,26 +239,29 @@ void sim_kernel(const SimArgs a) {
         // chunks pend_idx-2 and pend_idx-1. pc advances <= WCHUNK per WCHUNK rounds, so
         // the chunks read until the next refill point (pc/WCHUNK, pc/WCHUNK + 1) are
         // always resident; the pending chunk's load has WCHUNK rounds to land.
-        if ((r & (WCHUNK - 1)) == 0) {
-            // quiescence is absorbing, so testing it every QCHECK rounds only adds
-            // idle rounds (no state changes, not counted in `rounds`)
-            const bool qpoint = (r & (DASH_QCHECK - 1)) == 0;
-            if (qpoint && vote(active) == 0) break;
+        if (k == 0) {
+            // quiescence is absorbing, so testing it once per trip only adds idle
+            // rounds (no state changes, not counted in `rounds`)
+            if (vote(active) == 0) {
+                done = true;
+                break;
+            }
             // a non-final tier stops a system soon after its first overflow: it will be
             // re-simulated from scratch at the next depth, its results here are void
-            if (!FINAL && qpoint) {
+            if (!FINAL) {
                 const uint64_t ovf = vote(maxd > RING * SLOT);
                 if (ovf != 0) {
                     COLD();
                     const bool stop = ((uint32_t)(ovf >> seg) & SEGMASK) != 0;
                     wmask &= ~vote(stop);
                     if (stop) {
+                        nonempty = false;
                         cq = 0;
-                        len = pc;
+                        lenx = pc;
                     }
                 }
             }
-            if (pend_idx < nch && pend_idx < pc / WCHUNK + WIN) {
+            if (pend_idx < nch && pend_idx < pc / (WCHUNK * PCU) + WIN) {
                 put_chunk(pend_idx, pend);
                 ++pend_idx;
                 if (pend_idx < nch) pend = tr[pend_idx];
@@ -268,11 +278,11 @@ void sim_kernel(const SimArgs a) {
             const uint32_t A = ((uint32_t)key & (P - 1)) | 1u, Bc = (uint32_t)(key >> 8) & (P - 1);
             bitI = 1u << (4 * ((t * A + Bc) & (P - 1)));
         }
-        const bool has_msg = (cq != 0) & !stall;
-        const uint32_t m = *reinterpret_cast<const uint32_t*>(ldsb + L::RNG * 4 + ((tq - cq) & RMASK) + lane * 4);
-        const uint32_t ins = lds16[L::WND * 2 + (pc % (WIN * WCHUNK)) * 64 + sw];
-        const bool do_issue = (cq == 0) & can_issue & !stall;
-        pc += do_issue ? 1u : 0u;
+        const bool has_msg = nonempty & !stall;
+        const uint32_t m = *reinterpret_cast<const uint32_t*>(ldsb + L::RNG * 4 + ((tq - cq) & RMASK));
+        const uint32_t ins = *reinterpret_cast<const uint16_t*>(ldsb + L::WND * 4 + (pc & (WIN * WCHUNK * PCU - 1)) + sw * 2);
+        const bool do_issue = !nonempty & can_issue & !stall;
+        pc += do_issue ? PCU : 0u;
         if constexpr (ARB)
             cq -= has_msg ? SLOT : 0u;
         else
@@ -285,8 +295,11 @@ void sim_kernel(const SimArgs a) {
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         // cacheIndex = blockIndex % CACHE_SIZE (ref :188)
         const uint32_t idx = CS ? b % (uint32_t)CS : (uint32_t)(a.cs_lut >> (4 * b)) & 15u;
-        uint16_t* const ent = lds16 + L::ENT * 2 + b * 64 + sw;
-        uint16_t* const cac = lds16 + L::CAC * 2 + idx * 64 + sw;
+        // the row offsets stay in VGPRs from the loads to the stores (no recomputation)
+        uint32_t eoff = b * 64 + sw, coff = idx * 64 + sw;
+        asm volatile("" : "+v"(eoff), "+v"(coff));
+        uint16_t* const ent = lds16 + L::ENT * 2 + eoff;
+        uint16_t* const cac = lds16 + L::CAC * 2 + coff;
         const uint32_t e16 = *ent;
         const uint32_t c16 = *cac;
         const uint32_t mty = m & 15u;
@@ -420,7 +433,7 @@ void sim_kernel(const SimArgs a) {
         // ref :364-379): a sender's slot is the receiver's tail plus the number of
         // bits below its own, and the receiver's capacity check (ref :754-761)
         // compares the receiver's count plus that rank with the ring depth.
-        lds[L::MQ + 2 * lane + 1] = tq | col | (cq << 8);  // tail | ring column | count << 16
+        lds[L::MQ + 2 * lane + 1] = tq | (cq << 8);  // tail (with ring column) | count << 16
         const uint32_t bitP = bitI << 1, bitB = bitI << 2;
         if (vP)
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -543,7 +556,7 @@ void sim_kernel(const SimArgs a) {
         const uint64_t v = wsum(head_lane ? hcnt[k] : 0u);
         if (lane == 0 && v) atomicAdd(&S[STAT_HIST + k], (unsigned long long)v);
     }
-    const uint64_t s_instr = wsum(report ? pc : 0u);
+    const uint64_t s_instr = wsum(report ? pc / PCU : 0u);
     const uint64_t s_rounds = wsum(head_lane ? rounds : 0u);
     const uint64_t m_rounds = wmax(head_lane ? rounds : 0u);
     const uint64_t s_sys = wsum(head_lane ? 1u : 0u);

@@ -141,6 +141,14 @@ def reduce_totals(elapsed, counters, device, world):
     return float(t.item()), [int(x) for x in c.tolist()]
 
 
+def digest_sum(digests):
+    """[sum of low 32 bits, sum of high 32 bits] of the per-system state digests: exact in
+    int64 up to 2^31 systems, and independent of how systems are sharded over ranks."""
+    import numpy as np
+    d = np.asarray(digests, dtype=np.uint64)
+    return [int((d & np.uint64(0xFFFFFFFF)).sum(dtype=np.uint64)), int((d >> np.uint64(32)).sum(dtype=np.uint64))]
+
+
 def read_profile(kind):
     """Per-launch counters of the first-tier sim_kernel from the committed rocprofv3
     PMC summary for this workload (tools/pmc_summary.py), or None."""
@@ -286,9 +294,13 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
 
+    # a checksum of the per-system state digests (sums of their 32-bit
+    # halves: order-free, so identical for any GPU count), read back after the timed region
+    dg = eng.read_results()[0]
+    dsum = digest_sum(dg)
     elapsed, totals = reduce_totals(
         elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
-                                  stats["dropped"]], torch.device("cuda", dev), world)
+                                  stats["dropped"]] + dsum, torch.device("cuda", dev), world)
 
     instr_per_step = world * M * 8 * args.len
     value = instr_per_step * args.steps / elapsed
@@ -346,7 +358,8 @@ def main():
             "tier_systems": stats["tier_systems"],
             "wave_rounds": stats["wave_rounds"],
             "totals": {"hist": totals[:13], "instructions_per_step": totals[13],
-                       "rounds_total": totals[14], "err_systems": totals[15], "dropped": totals[16]},
+                       "rounds_total": totals[14], "err_systems": totals[15], "dropped": totals[16],
+                       "digest_sum": totals[17:19]},
         }
         print(json.dumps(line), flush=True)
     eng.close()

@@ -31,7 +31,7 @@ def _worker(rank, world, port, out):
     base, count = bench.shard(rank, world, PER_RANK)
     r = oc.run_batch(SEED, base, count, num_procs=8, cache_size=4, length=LEN, threads=1)
     counters = r["hist"].tolist() + [r["instructions"], int(r["rounds"].sum()),
-                                     int((r["errors"] != 0).sum()), 0]
+                                     int((r["errors"] != 0).sum()), 0] + bench.digest_sum(r["digests"])
     elapsed, totals = bench.reduce_totals(float(rank + 1), counters, torch.device("cpu"), world)
     out[rank] = (elapsed, totals, r["digests"].tolist())
     dist.destroy_process_group()
@@ -45,8 +45,9 @@ def test_two_rank_shards_reduce_to_single_run():
         mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
         res = dict(out)
     single = oc.run_batch(SEED, 0, PER_RANK * world, num_procs=8, cache_size=4, length=LEN, threads=2)
+    import bench
     expect = single["hist"].tolist() + [single["instructions"], int(single["rounds"].sum()),
-                                        int((single["errors"] != 0).sum()), 0]
+                                        int((single["errors"] != 0).sum()), 0] + bench.digest_sum(single["digests"])
     for rank in range(world):
         elapsed, totals, _ = res[rank]
         assert elapsed == float(world)  # MAX over ranks

@@ -46,5 +46,6 @@ def test_two_ranks_match_one_process():
     assert d2["totals"]["hist"] == d1["totals"]["hist"]
     assert d2["totals"]["rounds_total"] == d1["totals"]["rounds_total"]
     assert d2["totals"]["err_systems"] == d1["totals"]["err_systems"]
+    assert d2["totals"]["digest_sum"] == d1["totals"]["digest_sum"]  # final states, order-free
     # value = all ranks' instructions / max-over-ranks time
     assert abs(d2["value"] - 4096 * 8 * 512 / (d2["ms_per_step"] / 1e3)) < 1e-6 * d2["value"]

@@ -1,0 +1,38 @@
+"""The committed GPU evidence against the oracle's full-size run (CPU only, no GPU needed).
+
+tests/golden/full_size.json holds the oracle's totals over ALL 2^20 systems of BASELINE
+configs[2] (uniform) and [3] (contention), made by tests/golden/make_full_size.py. The
+bench lines committed under profiles/r01/ were measured on an MI355X over exactly those
+workloads; their per-type histograms, round totals and error-system counts must equal the
+oracle's (bit-exact), so every committed headline number is a run with the reference's
+results. The live GPU check of the same fixture is
+test_gpu_parity.py::test_full_size_sampled_parity (adds the digest checksum).
+"""
+import json
+import pathlib
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+GOLD = json.loads((ROOT / "tests" / "golden" / "full_size.json").read_text())
+BENCH = {"uniform": "v19_bench_uniform_final.json", "contention": "v19_bench_contention.json"}
+
+
+def test_fixture_shape():
+    assert GOLD["systems"] == 1 << 20 and GOLD["num_procs"] == 8 and GOLD["instr_per_node"] == 4096
+    for kind in BENCH:
+        g = GOLD[kind]
+        assert g["instructions"] == (1 << 20) * 8 * 4096  # every instruction issued
+        assert len(g["hist"]) == 13 and len(g["digest_sum"]) == 2
+
+
+@pytest.mark.parametrize("kind", list(BENCH))
+def test_committed_gpu_bench_matches_oracle(kind):
+    line = json.loads((ROOT / "profiles" / "r01" / BENCH[kind]).read_text())
+    assert line["config"]["systems_per_gpu"] == GOLD["systems"] and line["n_gpus"] == 1
+    assert line["config"]["trace"] == kind and line["config"]["cache_size"] == GOLD["cache_size"]
+    tot, g = line["totals"], GOLD[kind]
+    assert tot["hist"] == g["hist"]
+    assert tot["instructions_per_step"] == g["instructions"]
+    assert tot["rounds_total"] == g["rounds_total"]
+    assert tot["err_systems"] == g["err_systems"]

@@ -4,6 +4,7 @@ Bar: bit-exact (integer/byte work). Compared per system: full final state of
 every node, per-type message histogram, lockstep round count, error bits and
 the 64-bit digest.
 """
+import json
 import os
 import pathlib
 import shutil
@@ -12,6 +13,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import bench
 from oracle_ctypes import GOLDEN, load_test_dir, run_batch, run_system
 import oracle_ctypes
 
@@ -348,7 +350,10 @@ def test_full_size_sampled_parity(dash, kind):
     properties: every instruction issued, per-system statistics consistent with the
     totals, a run started one queue-depth tier deeper gives the same digest of every
     system (checksum of checksums), and 48 sampled systems are bit-exact (digest,
-    rounds, error bits) against the oracle."""
+    rounds, error bits) against the oracle. The whole run is bit-exact against the oracle's
+    own full-size run (tests/golden/full_size.json, made by tests/golden/make_full_size.py):
+    per-type histogram, round and error-system totals, and the order-free sums of all 2^20
+    per-system state digests."""
     N, CS, L, nsys, seed = 8, 4, 4096, 1 << 20, 0x5EED
     runs = []
     for flags in (0, dash.TIER_FROM_32):
@@ -362,6 +367,12 @@ def test_full_size_sampled_parity(dash, kind):
     assert st["err_systems"] == int(np.count_nonzero(err))
     assert np.array_equal(dig, dig2) and np.array_equal(rnd, rnd2) and np.array_equal(err, err2)
     assert st["hist"] == st2["hist"]
+    gold = json.loads((GOLDEN.parent / "full_size.json").read_text())["contention" if kind else "uniform"]
+    assert st["hist"] == gold["hist"]
+    assert st["instructions"] == gold["instructions"]
+    assert st["rounds_total"] == gold["rounds_total"]
+    assert st["err_systems"] == gold["err_systems"]
+    assert bench.digest_sum(dig) == gold["digest_sum"]
     rng = np.random.default_rng(kind)
     for s in sorted(rng.choice(nsys, 48, replace=False).tolist()):
         ref = run_batch(seed, s, 1, num_procs=N, cache_size=CS, length=L, kind=kind, threads=1)

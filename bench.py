@@ -218,6 +218,59 @@ def sweep(args, dash, rank, world, dev):
         dist.destroy_process_group()
 
 
+def host_traces(args, dash, rank, world, dev):
+    """PCIe-inclusive rate of the host-buffer boundary: per step, dash_load_traces (one strided
+    H2D copy of the caller's [system][node][instr] u16 array) plus the run. Synthetic uniform
+    traces from numpy's generator (node, block, R/W, value uniform; RD value 0)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    M, L = args.systems, args.len
+    rng = np.random.default_rng(args.seed + rank)
+    packed = rng.bit_generator.random_raw(M * 8 * L // 4).view(np.uint16).reshape(M, 8, L)
+    flat = packed.reshape(-1)
+    for i in range(0, flat.size, 1 << 26):  # RD carries value 0 (ref :839)
+        blk = flat[i:i + (1 << 26)]
+        blk &= (blk >> 15) * np.uint16(0xFF) | np.uint16(0xFF00)
+    lens = np.full((M, 8), L, dtype=np.uint32)
+    eng = dash.Engine(M, num_procs=8, cache_size=args.cache_size, max_instr=L, device=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        eng.load_traces(packed, lens)
+        eng.run()
+    barrier()
+    t0 = time.perf_counter()
+    load_s, kernel_ms = [], []
+    for _ in range(args.steps):
+        t1 = time.perf_counter()
+        eng.load_traces(packed, lens)
+        load_s.append(time.perf_counter() - t1)
+        kernel_ms.append(eng.run()["kernel_ms"])
+    barrier()
+    elapsed, _ = reduce_totals(time.perf_counter() - t0, [0], torch.device("cuda", dev), world)
+    instr = world * M * 8 * L * args.steps
+    if rank == 0:
+        print(json.dumps({"metric": "simulated instr/sec from host trace buffers (PCIe-inclusive), 8-core DASH systems",
+                          "value": instr / elapsed, "unit": "instr/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "dtype": "u8",
+                          "data": "synthetic host traces (numpy PCG64 raw bits, uniform-like)",
+                          "config": {"workload": f"{M} systems/GPU x 8 nodes x {L} instr, CACHE_SIZE={args.cache_size}, "
+                                                 f"traces handed over in host memory every step",
+                                     "trace_bytes_per_step": M * 8 * L * 2},
+                          "load_s_steps": [round(x, 4) for x in load_s],
+                          "h2d_GBps": M * 8 * L * 2 / (sum(load_s) / len(load_s)) / 1e9,
+                          "kernel_ms_steps": [round(x, 3) for x in kernel_ms]}), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -242,6 +295,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only for the "
                          "1-GPU rehearsal of the distributed path in tests/test_gpu_distributed.py)")
+    ap.add_argument("--host-traces", action="store_true",
+                    help="drop-in host-buffer path: traces built in host memory (numpy, uniform-like) and "
+                         "handed over through dash_load_traces inside every timed step (PCIe-inclusive rate; "
+                         "DESIGN.md §4); not the headline `value`")
     ap.add_argument("--sweep", action="store_true",
                     help="BASELINE configs[4]: CACHE_SIZE {1,2,4,8,16} x locality {0,.25,.5,.75,1}, "
                          "systems sharded over the ranks, histograms all-reduced per configuration")
@@ -266,6 +323,8 @@ def main():
 
     if args.sweep:
         return sweep(args, dash, rank, world, dev)
+    if args.host_traces:
+        return host_traces(args, dash, rank, world, dev)
 
     kind = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
             "locality": dash.GEN_LOCALITY}[args.kind]

@@ -213,27 +213,42 @@ int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const u
     for (uint64_t i = 0; i < num_systems * N; i++)
         if (lens[i] > h->cfg.max_instr || lens[i] > stride)
             return fail(h, DASH_EINVAL, "trace %llu longer than max_instr", (unsigned long long)i);
+    // the 3-bit node field cannot name a node >= 8, so only N < 8 needs the address scan
+    if (N < 8)
+        for (uint64_t r = 0; r < num_systems * N; r++)
+            for (uint32_t i = 0; i < lens[r]; i++) {
+                const uint16_t w = packed[r * stride + i];
+                if (((w >> 12) & 7u) >= N)
+                    return fail(h, DASH_EADDR, "system %llu node %u: address 0x%02X homed on node >= %u",
+                                (unsigned long long)(r / N), (unsigned)(r % N), (w >> 8) & 0x7F, N);
+            }
     // lane-contiguous layout: [group][lane][chunk][4 x u16]
     const uint64_t words = h->groups * (uint64_t)h->nchunks * 64;
     constexpr uint32_t C = dash::CHUNK_INSTR;
-    std::vector<uint16_t> host(words * C, 0);
-    for (uint64_t s = 0; s < num_systems; s++) {
-        const uint64_t g = s / (64 / P);
-        const uint32_t lane0 = (uint32_t)(s % (64 / P)) * P;
-        for (uint32_t t = 0; t < N; t++) {
-            const uint16_t* src = packed + (s * N + t) * stride;
-            for (uint32_t i = 0; i < lens[s * N + t]; i++) {
-                const uint16_t w = src[i];
-                if (((w >> 12) & 7u) >= N)
-                    return fail(h, DASH_EADDR, "system %llu node %u: address 0x%02X homed on node >= %u",
-                                (unsigned long long)s, t, (w >> 8) & 0x7F, N);
-                host[((g * 64 + lane0 + t) * h->nchunks + i / C) * C + (i % C)] = w;
+    const uint64_t pitch = (uint64_t)h->nchunks * 8;  // lane stride in bytes
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    if (P == N) {
+        // system s node t is lane row s*N + t in both layouts: one strided H2D copy, no
+        // host staging. Words past a node's length are never issued (the kernel's pc < len
+        // guard), so they need no zeroing.
+        if (num_systems)
+            HIPCHK(h, hipMemcpy2DAsync(h->d_trace, pitch, packed, stride * 2, std::min<uint64_t>(stride * 2, pitch),
+                                       num_systems * N, hipMemcpyHostToDevice, h->stream));
+    } else {
+        std::vector<uint16_t> host(words * C, 0);
+        for (uint64_t s = 0; s < num_systems; s++) {
+            const uint64_t g = s / (64 / P);
+            const uint32_t lane0 = (uint32_t)(s % (64 / P)) * P;
+            for (uint32_t t = 0; t < N; t++) {
+                const uint16_t* src = packed + (s * N + t) * stride;
+                for (uint32_t i = 0; i < lens[s * N + t]; i++)
+                    host[((g * 64 + lane0 + t) * h->nchunks + i / C) * C + (i % C)] = src[i];
             }
         }
+        if (words)
+            HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 8, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));  // `host` is pageable and local
     }
-    HIPCHK(h, hipSetDevice(h->cfg.device));
-    if (words)
-        HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 8, hipMemcpyHostToDevice, h->stream));
     if (num_systems)
         HIPCHK(h, hipMemcpyAsync(h->d_lens, lens, num_systems * N * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, reset_hint(h));

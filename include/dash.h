@@ -145,7 +145,9 @@ void dash_destroy(dash_t *h);
 const char *dash_last_error(const dash_t *h);
 
 /* traces: packed u16 (bit15 = WR, bits 14..8 = address, bits 7..0 = value),
-   layout [sys][node][stride]; lens[sys*num_procs + node] */
+   layout [sys][node][stride]; lens[sys*num_procs + node]. Synchronous: the caller's
+   buffer is read (for power-of-two num_procs, by one strided H2D copy) before return;
+   words at or past a node's length are never simulated. */
 int dash_load_traces(dash_t *h, const uint16_t *packed, uint64_t stride, const uint32_t *lens,
                      uint64_t num_systems);
 int dash_generate(dash_t *h, const dash_gen *g);

@@ -221,7 +221,11 @@ def sweep(args, dash, rank, world, dev):
 def host_traces(args, dash, rank, world, dev):
     """PCIe-inclusive rate of the host-buffer boundary: per step, dash_load_traces (one strided
     H2D copy of the caller's [system][node][instr] u16 array) plus the run. Synthetic uniform
-    traces from numpy's generator (node, block, R/W, value uniform; RD value 0)."""
+    traces from numpy's generator (node, block, R/W, value uniform; RD value 0). With
+    --host-batches B > 1 the systems go in B equal batches through two dash_t handles (each
+    with its own HIP stream) on two host threads: batch k+1's copy overlaps batch k's run."""
+    import threading
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -233,7 +237,33 @@ def host_traces(args, dash, rank, world, dev):
         blk = flat[i:i + (1 << 26)]
         blk &= (blk >> 15) * np.uint16(0xFF) | np.uint16(0xFF00)
     lens = np.full((M, 8), L, dtype=np.uint32)
-    eng = dash.Engine(M, num_procs=8, cache_size=args.cache_size, max_instr=L, device=dev)
+    B = args.host_batches
+    if B < 1 or M % B:
+        raise SystemExit("--host-batches must divide --systems")
+    Mb = M // B
+    engs = [dash.Engine(Mb, num_procs=8, cache_size=args.cache_size, max_instr=L, device=dev)
+            for _ in range(min(B, 2))]
+    hist = np.zeros(13, dtype=np.uint64)
+    load_s, kernel_ms = [], []
+    lock = threading.Lock()
+
+    def lane(i):  # host thread i drives handle i over batches i, i+2, ... (ctypes drops the GIL)
+        torch.cuda.set_device(dev)
+        for b in range(i, B, len(engs)):
+            t1 = time.perf_counter()
+            engs[i].load_traces(packed[b * Mb:(b + 1) * Mb], lens[b * Mb:(b + 1) * Mb])
+            load_s.append(time.perf_counter() - t1)
+            st = engs[i].run()
+            with lock:
+                kernel_ms.append(st["kernel_ms"])
+                hist[:] += np.array(st["hist"], dtype=np.uint64)
+
+    def step():
+        ts = [threading.Thread(target=lane, args=(i,)) for i in range(len(engs))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
 
     def barrier():
         if world > 1:
@@ -241,16 +271,14 @@ def host_traces(args, dash, rank, world, dev):
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        eng.load_traces(packed, lens)
-        eng.run()
+        step()
     barrier()
+    hist[:] = 0
+    load_s.clear()
+    kernel_ms.clear()
     t0 = time.perf_counter()
-    load_s, kernel_ms = [], []
     for _ in range(args.steps):
-        t1 = time.perf_counter()
-        eng.load_traces(packed, lens)
-        load_s.append(time.perf_counter() - t1)
-        kernel_ms.append(eng.run()["kernel_ms"])
+        step()
     barrier()
     elapsed, _ = reduce_totals(time.perf_counter() - t0, [0], torch.device("cuda", dev), world)
     instr = world * M * 8 * L * args.steps
@@ -262,11 +290,13 @@ def host_traces(args, dash, rank, world, dev):
                           "data": "synthetic host traces (numpy PCG64 raw bits, uniform-like)",
                           "config": {"workload": f"{M} systems/GPU x 8 nodes x {L} instr, CACHE_SIZE={args.cache_size}, "
                                                  f"traces handed over in host memory every step",
-                                     "trace_bytes_per_step": M * 8 * L * 2},
+                                     "trace_bytes_per_step": M * 8 * L * 2, "host_batches": B},
                           "load_s_steps": [round(x, 4) for x in load_s],
-                          "h2d_GBps": M * 8 * L * 2 / (sum(load_s) / len(load_s)) / 1e9,
+                          "h2d_GBps": M * 8 * L * 2 * args.steps / sum(load_s) / 1e9,
+                          "hist_per_step": [int(x) // args.steps for x in hist],
                           "kernel_ms_steps": [round(x, 3) for x in kernel_ms]}), flush=True)
-    eng.close()
+    for e in engs:
+        e.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -299,6 +329,9 @@ def main():
                     help="drop-in host-buffer path: traces built in host memory (numpy, uniform-like) and "
                          "handed over through dash_load_traces inside every timed step (PCIe-inclusive rate; "
                          "DESIGN.md §4); not the headline `value`")
+    ap.add_argument("--host-batches", type=int, default=1,
+                    help="--host-traces: split the systems into this many batches on two handles driven by two "
+                         "host threads, so one batch's H2D copy overlaps another's simulation")
     ap.add_argument("--sweep", action="store_true",
                     help="BASELINE configs[4]: CACHE_SIZE {1,2,4,8,16} x locality {0,.25,.5,.75,1}, "
                          "systems sharded over the ranks, histograms all-reduced per configuration")

@@ -1,0 +1,32 @@
+"""The host-buffer boundary as bench.py drives it (--host-traces): traces handed over from host
+memory through dash_load_traces every step, unbatched and in batches on two handles driven
+by two host threads (copies overlapped with runs). Batching must not change any result:
+the per-type histograms of the same host traces are identical for B = 1, 4 and 8."""
+import json
+import pathlib
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+ARGS = ["--host-traces", "--systems", "4096", "--len", "512", "--steps", "1", "--warmup", "1"]
+
+
+def _run(batches):
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py")] + ARGS + ["--host-batches", str(batches)],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+
+
+def test_batched_host_path_matches_unbatched():
+    one = _run(1)
+    assert sum(one["hist_per_step"]) > 0 and one["config"]["host_batches"] == 1
+    assert one["value"] > 0 and one["h2d_GBps"] > 0
+    for b in (4, 8):
+        d = _run(b)
+        assert d["config"]["host_batches"] == b
+        assert d["hist_per_step"] == one["hist_per_step"], b
+        assert len(d["load_s_steps"]) == b and len(d["kernel_ms_steps"]) == b

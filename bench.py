@@ -259,6 +259,12 @@ def host_traces(args, dash, rank, world, dev):
                 hist[:] += np.array(st["hist"], dtype=np.uint64)
 
     def step():
+        if args.host_native:
+            st = dash.run_host_batched(packed, lens, B, num_procs=8, cache_size=args.cache_size, device=dev)[0]
+            with lock:
+                kernel_ms.append(st["kernel_ms"])
+                hist[:] += np.array(st["hist"], dtype=np.uint64)
+            return
         ts = [threading.Thread(target=lane, args=(i,)) for i in range(len(engs))]
         for t in ts:
             t.start()
@@ -290,9 +296,10 @@ def host_traces(args, dash, rank, world, dev):
                           "data": "synthetic host traces (numpy PCG64 raw bits, uniform-like)",
                           "config": {"workload": f"{M} systems/GPU x 8 nodes x {L} instr, CACHE_SIZE={args.cache_size}, "
                                                  f"traces handed over in host memory every step",
-                                     "trace_bytes_per_step": M * 8 * L * 2, "host_batches": B},
+                                     "trace_bytes_per_step": M * 8 * L * 2, "host_batches": B,
+                                     "driver": "dash_run_host_batched" if args.host_native else "python threads"},
                           "load_s_steps": [round(x, 4) for x in load_s],
-                          "h2d_GBps": M * 8 * L * 2 * args.steps / sum(load_s) / 1e9,
+                          "h2d_GBps": M * 8 * L * 2 * args.steps / sum(load_s) / 1e9 if load_s else None,
                           "hist_per_step": [int(x) // args.steps for x in hist],
                           "kernel_ms_steps": [round(x, 3) for x in kernel_ms]}), flush=True)
     for e in engs:
@@ -332,6 +339,9 @@ def main():
     ap.add_argument("--host-batches", type=int, default=1,
                     help="--host-traces: split the systems into this many batches on two handles driven by two "
                          "host threads, so one batch's H2D copy overlaps another's simulation")
+    ap.add_argument("--host-native", action="store_true",
+                    help="--host-traces through the library's own batched entry point (dash_run_host_batched: "
+                         "C++ threads, handles created per call) instead of Python threads over two engines")
     ap.add_argument("--sweep", action="store_true",
                     help="BASELINE configs[4]: CACHE_SIZE {1,2,4,8,16} x locality {0,.25,.5,.75,1}, "
                          "systems sharded over the ranks, histograms all-reduced per configuration")

@@ -150,6 +150,15 @@ const char *dash_last_error(const dash_t *h);
    words at or past a node's length are never simulated. */
 int dash_load_traces(dash_t *h, const uint16_t *packed, uint64_t stride, const uint32_t *lens,
                      uint64_t num_systems);
+/* Host-buffer throughput path (replaces the same load+run for callers whose traces sit in
+   host memory): num_systems (a multiple of batches) go through in `batches` equal batches
+   on two handles made from *cfg (num_systems = the batch size), each driven by its own host
+   thread and HIP stream, so one batch's H2D copy overlaps another's run. Results equal one
+   dash_load_traces + dash_run over all systems: merged *stats (kernel_ms = sum over
+   batches), and per-system digests / rounds / errors into the optional arrays. */
+int dash_run_host_batched(const dash_cfg *cfg, const uint16_t *packed, uint64_t stride,
+                          const uint32_t *lens, uint64_t num_systems, uint32_t batches,
+                          dash_stats *stats, uint64_t *digests, uint32_t *rounds, uint32_t *errors);
 int dash_generate(dash_t *h, const dash_gen *g);
 int dash_run(dash_t *h, dash_stats *stats);
 int dash_read_state(dash_t *h, uint64_t sys, dash_node_state *out /* [num_procs] */);

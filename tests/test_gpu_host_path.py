@@ -30,3 +30,24 @@ def test_batched_host_path_matches_unbatched():
         assert d["config"]["host_batches"] == b
         assert d["hist_per_step"] == one["hist_per_step"], b
         assert len(d["load_s_steps"]) == b and len(d["kernel_ms_steps"]) == b
+
+
+@pytest.mark.parametrize("N,batches", [(8, 1), (8, 4), (8, 8), (4, 2), (5, 3)])
+def test_run_host_batched_matches_single_run(dash, N, batches):
+    """dash_run_host_batched (two handles, two host threads, copies overlapped with runs)
+    gives exactly the per-system results and merged statistics of one dash_load_traces +
+    dash_run over all systems (N = 5 takes the host re-layout path)."""
+    import numpy as np
+    from test_gpu_parity import random_batch
+    rng = np.random.default_rng(77 + N * 10 + batches)
+    packed, lens = random_batch(rng, 96 * batches, N, 120, hot_frac=0.2)
+    st, d, r, e = dash.run_host_batched(packed, lens, batches, num_procs=N, cache_size=4)
+    with dash.Engine(packed.shape[0], num_procs=N, cache_size=4, max_instr=packed.shape[2]) as eng:
+        eng.load_traces(packed, lens)
+        st1 = eng.run()
+        d1, r1, e1 = eng.read_results()
+    assert np.array_equal(d, d1) and np.array_equal(r, r1) and np.array_equal(e, e1)
+    for k in ("hist", "instructions", "rounds_total", "rounds_max", "systems", "err_systems", "err_bits",
+              "dropped", "max_depth"):
+        assert st[k] == st1[k], k
+    assert st["instructions"] == int(lens.sum())

@@ -623,3 +623,76 @@ int dash_simulate_dir(const char* dir, uint32_t num_procs, uint32_t cache_size, 
 }
 
 }  // extern "C"
+
+// ---- host-buffer throughput path: batches on two handles, copies overlapped with runs ----
+extern "C" int dash_run_host_batched(const dash_cfg* cfg, const uint16_t* packed, uint64_t stride,
+                                     const uint32_t* lens, uint64_t num_systems, uint32_t batches,
+                                     dash_stats* stats, uint64_t* digests, uint32_t* rounds,
+                                     uint32_t* errors) {
+    if (!cfg || !packed || !lens || !stats || batches == 0 || num_systems == 0 || num_systems % batches)
+        return DASH_EINVAL;
+    const uint64_t nb = num_systems / batches, N = cfg->num_procs;
+    dash_cfg c = *cfg;
+    c.num_systems = nb;
+    const unsigned nh = batches < 2 ? 1u : 2u;
+    dash_t* h[2] = {nullptr, nullptr};
+    int rc = DASH_OK;
+    for (unsigned i = 0; i < nh && rc == DASH_OK; i++) rc = dash_create(&c, &h[i]);
+    dash_stats part[2];
+    memset(part, 0, sizeof part);
+    int trc[2] = {DASH_OK, DASH_OK};
+    // handle i (its own HIP stream) takes batches i, i+2, ...: while one copies, the other runs
+    auto lane = [&](unsigned i) {
+        for (uint64_t b = i; b < batches && trc[i] == DASH_OK; b += nh) {
+            int r = dash_load_traces(h[i], packed + b * nb * N * stride, stride, lens + b * nb * N, nb);
+            dash_stats st;
+            if (r == DASH_OK) r = dash_run(h[i], &st);
+            if (r == DASH_OK && (digests || rounds || errors))
+                r = dash_read_results(h[i], 0, nb, digests ? digests + b * nb : nullptr,
+                                      rounds ? rounds + b * nb : nullptr, errors ? errors + b * nb : nullptr);
+            if (r != DASH_OK) {
+                trc[i] = r;
+                break;
+            }
+            dash_stats& p = part[i];
+            for (int k = 0; k < DASH_NUM_TXN; k++) p.hist[k] += st.hist[k];
+            p.instructions += st.instructions;
+            p.rounds_total += st.rounds_total;
+            p.rounds_max = std::max(p.rounds_max, st.rounds_max);
+            p.systems += st.systems;
+            p.err_systems += st.err_systems;
+            p.err_bits |= st.err_bits;
+            p.dropped += st.dropped;
+            p.max_depth = std::max(p.max_depth, st.max_depth);
+            p.kernel_ms += st.kernel_ms;
+            for (int k = 0; k < DASH_NUM_TIERS; k++) p.tier_systems[k] += st.tier_systems[k];
+            p.wave_rounds += st.wave_rounds;
+        }
+    };
+    if (rc == DASH_OK) {
+        std::vector<std::thread> pool;
+        for (unsigned i = 0; i < nh; i++) pool.emplace_back(lane, i);
+        for (auto& t : pool) t.join();
+        rc = trc[0] != DASH_OK ? trc[0] : trc[1];
+    }
+    for (unsigned i = 0; i < nh; i++)
+        if (h[i]) dash_destroy(h[i]);
+    if (rc != DASH_OK) return rc;
+    *stats = part[0];
+    if (nh == 2) {
+        const dash_stats& q = part[1];
+        for (int k = 0; k < DASH_NUM_TXN; k++) stats->hist[k] += q.hist[k];
+        stats->instructions += q.instructions;
+        stats->rounds_total += q.rounds_total;
+        stats->rounds_max = std::max(stats->rounds_max, q.rounds_max);
+        stats->systems += q.systems;
+        stats->err_systems += q.err_systems;
+        stats->err_bits |= q.err_bits;
+        stats->dropped += q.dropped;
+        stats->max_depth = std::max(stats->max_depth, q.max_depth);
+        stats->kernel_ms += q.kernel_ms;
+        for (int k = 0; k < DASH_NUM_TIERS; k++) stats->tier_systems[k] += q.tier_systems[k];
+        stats->wave_rounds += q.wave_rounds;
+    }
+    return DASH_OK;
+}

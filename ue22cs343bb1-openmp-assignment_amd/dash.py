@@ -51,7 +51,7 @@ EXPORTS = ("dash_create", "dash_destroy", "dash_last_error", "dash_load_traces",
            "dash_parse_core_file", "dash_resolve_dir", "dash_load_dir", "dash_init_node_state",
            "dash_dump_node", "dash_dump_file", "dash_digest_node", "dash_simulate_dir",
            "dash_read_events", "dash_format_event", "dash_load_dirs", "dash_dump_system",
-           "dash_write_digests")
+           "dash_write_digests", "dash_run_host_batched")
 
 
 class DashError(RuntimeError):
@@ -144,6 +144,8 @@ def lib() -> ctypes.CDLL:
         "dash_dump_system": (i32, [vp, u64, ctypes.c_char_p]),
         "dash_write_digests": (i32, [vp, ctypes.c_char_p]),
         "dash_format_event": (i32, [ctypes.POINTER(Event), ctypes.c_char_p, ctypes.c_size_t]),
+        "dash_run_host_batched": (i32, [ctypes.POINTER(Cfg), vp, u64, vp, u64, u32, ctypes.POINTER(Stats),
+                                        vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -212,6 +214,25 @@ def simulate_dir(test_dir, out_dir=".", num_procs=4, cache_size=4, max_instr=32,
                                    str(out_dir).encode(), device, ctypes.byref(st)),
            f"simulate_dir {test_dir}")
     return st.as_dict()
+
+
+def run_host_batched(packed: np.ndarray, lens: np.ndarray, batches: int, num_procs=8, cache_size=4,
+                     max_instr=None, device=0, flags=0):
+    """dash_run_host_batched: host traces [systems, num_procs, stride] u16 in `batches` batches
+    on two handles, copies overlapped with runs. Returns (stats dict, digests, rounds, errors)."""
+    packed = np.ascontiguousarray(packed, dtype=np.uint16)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    nsys = packed.shape[0]
+    assert packed.ndim == 3 and packed.shape[1] == num_procs and lens.shape == (nsys, num_procs)
+    cfg = Cfg(num_procs, cache_size, max_instr or packed.shape[2], flags, nsys, 0, device, 0, 0)
+    st = Stats()
+    d = np.zeros(nsys, dtype=np.uint64)
+    r = np.zeros(nsys, dtype=np.uint32)
+    e = np.zeros(nsys, dtype=np.uint32)
+    _check(lib().dash_run_host_batched(ctypes.byref(cfg), packed.ctypes.data, packed.shape[2], lens.ctypes.data,
+                                       nsys, batches, ctypes.byref(st), d.ctypes.data, r.ctypes.data,
+                                       e.ctypes.data), "dash_run_host_batched")
+    return st.as_dict(), d, r, e
 
 
 # ------------------------------------------------------------------ device engine

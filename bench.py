@@ -13,6 +13,11 @@ with no data-path collective (weak scaling); the single exchange is one RCCL
 all-reduce of the per-transaction histograms after the timed region.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
+
+Other modes (not the headline): --kind contention (configs[3]); --sweep (configs[4]);
+--host-traces [--host-batches B] [--host-native]: traces handed over from host memory every
+step (PCIe-inclusive rate of the drop-in boundary); --cpu-kind reference:
+the reference binary itself as the CPU baseline.
 """
 import argparse
 import json

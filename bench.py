@@ -8,9 +8,17 @@ by the GLOBAL system id) before the timed region, so they are resident in
 HBM (64 GiB per GPU). One step = one full pass of the hot path: every system
 from initial state to quiescence.
 
-Multi-GPU: one process per GPU (torchrun). Systems are sharded by global id
-with no data-path collective (weak scaling); the single exchange is one RCCL
-all-reduce of the per-transaction histograms after the timed region.
+Multi-GPU: one process per GPU. `bench.py --gpus N` starts the N ranks itself (a parent
+that never touches the GPU spawns N fresh child processes with RANK / LOCAL_RANK /
+WORLD_SIZE set); under torchrun the ranks come from the environment and WORLD_SIZE must
+equal --gpus. Systems are sharded by global id with no data-path collective (weak
+scaling); the single exchange is one RCCL all-reduce of the per-transaction histograms
+after the timed region.
+
+The headline line also carries `contention` (BASELINE configs[3], its own timed steps),
+`cpu_baseline` (the reference itself, assignment.c + the SURVEY §8(d) benchmark patch,
+one instance per host core = BASELINE.md mode (A)) and `cpu_port` (the oracle restatement
+on the same host).
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 
@@ -34,7 +42,31 @@ BYTES_PER_INSTR = 2  # packed trace record read once
 # measured by tools/micro (profiles/r01/micro); the SIMD-32 issue limit of plain VOP2
 # forms in homogeneous streams is 2 per cycle per CU. 256 CUs x 2.4 GHz.
 VALU_PEAK = 256 * 2.4e9
+# architectural VALU issue limit (MI355X_MICROARCH.md "Wave scheduling": a wave64 VALU
+# instruction occupies a SIMD-32 for 2 cycles, 4 SIMDs per CU): 2 per cycle per CU
 VALU_PEAK_SIMD32 = 2 * VALU_PEAK
+
+
+def host_cores():
+    """CPUs this process may use: the cgroup CPU quota when one is set (the GPU box shows
+    hundreds of CPUs but grants a 16-CPU share), else the affinity mask."""
+    try:
+        quota, period = pathlib.Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_model():
+    try:
+        for ln in pathlib.Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def load_dash():
@@ -61,7 +93,7 @@ def cpu_baseline(args, seed, kind, locality, target_s):
     res = oc.run_batch(seed, 0, count, num_procs=8, cache_size=args.cache_size, length=args.len,
                        kind=kind, locality=locality, threads=threads)
     return {"value": res["instructions"] / res["seconds"], "unit": "instr/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{count} systems x 8 nodes x {args.len} instr ({args.kind}, CS={args.cache_size}, "
                       f"seed 0x{seed:X}) in {res['seconds']:.1f} s on {threads} threads; "
                       f"oracle/dash_oracle.c lockstep restatement of assignment.c"}
@@ -80,8 +112,9 @@ def ref_baseline(args, seed, kind_id, target_s):
     import oracle_ctypes as oc
     exe = ROOT / "oracle" / "_ref" / "cache_simulator_bench"
     if not exe.exists():
-        raise SystemExit(f"{exe} missing: build it with oracle/build_ref.sh where /root/reference exists")
-    k = args.ref_instances
+        raise RuntimeError(f"{exe.relative_to(ROOT)} missing (built by __graft_entry__.build() / "
+                           f"oracle/build_ref.sh where /root/reference exists)")
+    k = args.ref_instances or host_cores()
     with tempfile.TemporaryDirectory() as td:
         dirs = []
         for i in range(k):
@@ -102,16 +135,18 @@ def ref_baseline(args, seed, kind_id, target_s):
             while any(p.poll() is None for p in procs):  # spinning instances can take minutes
                 time.sleep(0.02)
                 now = time.perf_counter()
-                if now - tb > 900:
+                if now - tb > args.ref_timeout:
                     for p in procs:
                         p.kill()
-                    raise SystemExit("reference instances did not finish within 900 s")
+                    for p in procs:
+                        p.wait()
+                    raise RuntimeError(f"reference instances did not finish within {args.ref_timeout:.0f} s")
                 if now - last > 30:
                     last = now
                     print(f"[ref_baseline] {sum(p.poll() is not None for p in procs)}/{k} instances done, "
                           f"{now - tb:.0f} s", file=sys.stderr, flush=True)
             if any(p.returncode != 0 for p in procs):
-                raise SystemExit(f"reference instance exited with {[p.returncode for p in procs]}")
+                raise RuntimeError(f"reference instance exited with {[p.returncode for p in procs]}")
             batches += 1
             elapsed = time.perf_counter() - t0
             if elapsed >= target_s:
@@ -119,12 +154,14 @@ def ref_baseline(args, seed, kind_id, target_s):
         for d in dirs:  # every instance reached quiescence and dumped its 8 nodes
             assert all((d / f"core_{n}_output.txt").exists() for n in range(8)), d
     instr = batches * k * 8 * args.len
-    cores = min(len(os.sched_getaffinity(0)), args.cpu_threads)
+    cores = host_cores()
     return {"value": instr / elapsed, "unit": "instr/s", "cores": cores, "kind": "reference",
+            "mode": "A" if k == cores else ("B" if k == 1 else f"{k} instances"),
+            "cpu_model": cpu_model(),
             "sample": f"{batches} batch(es) x {k} concurrent instance(s) x 8 OpenMP threads, one 8-node system "
                       f"x {args.len} instr each ({args.kind}, CS=4, systems 0..{k - 1} of seed 0x{seed:X}) "
-                      f"in {elapsed:.1f} s; assignment.c + benchmark patch (oracle/patch_ref.py), "
-                      f"gcc -O2 -fopenmp"}
+                      f"in {elapsed:.1f} s on {cores} host cores ({cpu_model()}); assignment.c + benchmark "
+                      f"patch (oracle/patch_ref.py), gcc -O2 -fopenmp"}
 
 
 def shard(rank, world, per_gpu):
@@ -200,15 +237,18 @@ def sweep(args, dash, rank, world, dev):
             eng.generate(args.seed, args.len, kind=dash.GEN_LOCALITY, locality=int(round(p * 65536)),
                          sys_base=sys_base)
             elapsed, stats = timed_runs(eng, args, world, dev)
+            dsum = digest_sum(eng.read_results()[0])
             elapsed, totals = reduce_totals(
                 elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
-                                          stats["dropped"]], torch.device("cuda", dev), world)
+                                          stats["dropped"]] + dsum, torch.device("cuda", dev), world)
             eng.close()
             points.append({"cache_size": cs, "locality": p,
                            "value": world * M * 8 * args.len * args.steps / elapsed,
                            "ms_per_step": elapsed / args.steps * 1e3,
+                           "kernel_ms": stats["kernel_ms"],
                            "rounds_per_system": totals[14] / (world * M),
-                           "hist": totals[:13], "err_systems": totals[15],
+                           "hist": totals[:13], "instructions": totals[13], "rounds_total": totals[14],
+                           "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19],
                            "tier_systems": stats["tier_systems"]})
     if rank == 0:
         print(json.dumps({"metric": "simulated instr/sec (whole node), 8-core DASH systems; sweep",
@@ -313,9 +353,130 @@ def host_traces(args, dash, rank, world, dev):
         dist.destroy_process_group()
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` without torchrun: start N ranks as fresh child processes (this
+    parent never initialises HIP, so nothing is exec'd from a GPU process), one per GPU,
+    with the torch.distributed environment set; rank 0 prints the line. Any rank failing
+    stops the others and fails the launch."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(pathlib.Path(__file__).resolve())] + sys.argv[1:],
+                                      env=env, start_new_session=True))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:  # one rank failed: the collectives of the others would hang
+                        os.killpg(q.pid, signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                os.killpg(q.pid, signal.SIGKILL)
+    return rc
+
+
+def timed_headline(eng, args, world, dev):
+    """W untimed steps, then exactly K timed steps bracketed by barrier + synchronize."""
+    import torch
+    import torch.distributed as dist
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        eng.run()
+    barrier()
+    t0 = time.perf_counter()
+    kernel_ms = []
+    stats = None
+    for _ in range(args.steps):
+        stats = eng.run()
+        kernel_ms.append(stats["kernel_ms"])
+    barrier()
+    return time.perf_counter() - t0, stats, kernel_ms
+
+
+def roofline(M, args, avg_kernel_s, prof):
+    """Algorithmic bytes per launch (2 B per simulated instruction) over the
+    launch's average duration (HIP events on the engine's stream), against 8 TB/s;
+    `traffic` = HBM bytes per launch of the same kernel from the committed rocprofv3 PMC
+    run (profiles/pmc_<kind>.json, tools/pmc_summary.py), not from this process."""
+    achieved = M * 8 * args.len * BYTES_PER_INSTR / avg_kernel_s
+    return {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+            "frac": achieved / PEAK_HBM, "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
+            "traffic_source": (f"{prof.get('source')} (committed rocprofv3 --pmc run of this kernel, "
+                               f"per launch)") if prof else None}
+
+
+def valu_issue(prof, wave_rounds):
+    """Issue figures of the first-tier launch from its committed PMC run (count / duration),
+    against the architectural 2 wave64 VALU per cycle per CU (so frac <= 1)."""
+    if not prof:
+        return None
+    rate = prof["valu_per_launch"] / (prof["kernel_ms"] / 1e3)
+    wr = max(wave_rounds, 1)
+    return {"achieved": rate, "peak": VALU_PEAK_SIMD32, "unit": "wave-instr/s", "frac": rate / VALU_PEAK_SIMD32,
+            "peak_basis": "2 wave64 VALU/cycle/CU x 256 CUs x 2.4 GHz (MI355X_MICROARCH.md wave scheduling)",
+            "valu_per_wave_round": prof["valu_per_launch"] / wr,
+            "salu_per_wave_round": prof.get("sq_insts_salu", 0.0) / wr,
+            "lds_per_wave_round": prof.get("sq_insts_lds", 0.0) / wr,
+            "lds_bank_conflict_frac": (prof["sq_lds_bank_conflict"] / prof["sq_lds_idx_active"]
+                                       if prof.get("sq_lds_idx_active") else None),
+            "l2_hit_rate": prof.get("l2_hit_rate"),
+            "source": f"{prof.get('source')} (committed rocprofv3 --pmc run, not this process)"}
+
+
+def run_kind(dash, args, kind_name, M, sys_base, world, dev, steps, tier_flag):
+    """One workload (uniform / contention / locality): generate on the device, time it,
+    all-reduce the totals; returns (elapsed, totals, stats, kernel_ms)."""
+    import torch
+    kind = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
+            "locality": dash.GEN_LOCALITY}[kind_name]
+    locality = int(round(args.locality * 65536)) if kind_name == "locality" else 0
+    eng = dash.Engine(M, num_procs=8, cache_size=args.cache_size, max_instr=args.len,
+                      device=dev, flags=tier_flag)
+    try:
+        eng.generate(args.seed, args.len, kind=kind, locality=locality, sys_base=sys_base)
+        a = argparse.Namespace(**vars(args))
+        a.steps = steps
+        elapsed, stats, kernel_ms = timed_headline(eng, a, world, dev)
+        # SURVEY.md §8(e): a checksum of the per-system state digests (sums of their 32-bit
+        # halves: order-free, so identical for any GPU count), read back after the timed region
+        dsum = digest_sum(eng.read_results()[0])
+    finally:
+        eng.close()
+    elapsed, totals = reduce_totals(
+        elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
+                                  stats["dropped"]] + dsum, torch.device("cuda", dev), world)
+    return elapsed, totals, stats, kernel_ms
+
+
+def totals_dict(totals):
+    return {"hist": totals[:13], "instructions_per_step": totals[13], "rounds_total": totals[14],
+            "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19]}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without torchrun bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--systems", type=int, default=1 << 20, help="systems per GPU")
@@ -324,14 +485,20 @@ def main():
     ap.add_argument("--kind", choices=["uniform", "contention", "locality"], default="uniform")
     ap.add_argument("--locality", type=float, default=0.5)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
+    ap.add_argument("--contention-steps", type=int, default=5,
+                    help="timed steps of the contention workload (configs[3]) reported in the headline "
+                         "line's `contention` object (0 = skip); its own warmup step precedes them")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-kind", choices=["port", "reference"], default="port",
-                    help="cpu_baseline leg: the oracle port on --cpu-threads threads, or the reference "
-                         "binary itself (oracle/_ref/cache_simulator_bench)")
-    ap.add_argument("--ref-instances", type=int, default=1,
-                    help="concurrent reference instances for --cpu-kind reference")
+    ap.add_argument("--cpu-kind", choices=["port", "reference"], default="reference",
+                    help="headline cpu_baseline: the reference binary itself (oracle/_ref/cache_simulator_bench, "
+                         "default; the oracle port is then reported as cpu_port) or only the oracle port")
+    ap.add_argument("--ref-instances", type=int, default=0,
+                    help="concurrent reference instances (0 = one per host core: BASELINE.md mode (A); "
+                         "1 = mode (B))")
+    ap.add_argument("--ref-timeout", type=float, default=240.0,
+                    help="give up on the reference baseline after this many seconds (reported as null)")
     ap.add_argument("--first-depth", type=int, choices=[0, 32, 256], default=0,
                     help="first queue-depth tier (0 = adaptive, starting at 16)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -350,18 +517,45 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="BASELINE configs[4]: CACHE_SIZE {1,2,4,8,16} x locality {0,.25,.5,.75,1}, "
                          "systems sharded over the ranks, histograms all-reduced per configuration")
+    ap.add_argument("--dist-selftest", action="store_true",
+                    help="no GPU: the rank launch plus one gloo all-reduce of the shard table on the CPU "
+                         "(tests/test_distributed.py checks the launcher with it)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: the rank count must equal --gpus")
 
     import torch
     import torch.distributed as dist
 
+    if args.dist_selftest:  # CPU only: what each rank owns, summed over the ranks
+        if world > 1:
+            dist.init_process_group("gloo")
+        base, count = shard(rank, world, args.systems)
+        owned = torch.zeros(world * args.systems, dtype=torch.int64)
+        owned[base:base + count] = 1
+        if world > 1:
+            dist.all_reduce(owned)
+        if rank == 0:
+            print(json.dumps({"world": world, "systems_owned": int(owned.sum()),
+                              "each_once": bool((owned == 1).all()), "local_rank": local_rank}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     dash = load_dash()
-    # one rank per GPU; ranks beyond the visible GPUs share them (rehearsal only)
-    dev = local_rank % max(torch.cuda.device_count(), 1)
+    # one rank per GPU; ranks beyond the visible GPUs share them (1-GPU rehearsal, gloo only)
+    ndev = torch.cuda.device_count()
+    if world > ndev and args.dist_backend == "nccl":
+        raise SystemExit(f"bench.py: {world} ranks over nccl need {world} GPUs, {ndev} visible")
+    dev = local_rank % max(ndev, 1)
     torch.cuda.set_device(dev)
     if world > 1:
         if args.dist_backend == "nccl":
@@ -374,56 +568,51 @@ def main():
     if args.host_traces:
         return host_traces(args, dash, rank, world, dev)
 
-    kind = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
-            "locality": dash.GEN_LOCALITY}[args.kind]
-    locality = int(round(args.locality * 65536)) if args.kind == "locality" else 0
-    M = args.systems
     tier_flag = {0: 0, 32: dash.TIER_FROM_32, 256: dash.TIER_FROM_256}[args.first_depth]
-    eng = dash.Engine(M, num_procs=8, cache_size=args.cache_size, max_instr=args.len,
-                      device=dev, flags=tier_flag)
-    sys_base, M = shard(rank, world, M)
-    eng.generate(args.seed, args.len, kind=kind, locality=locality, sys_base=sys_base)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        eng.run()
-    barrier()
-    t0 = time.perf_counter()
-    kernel_ms = []
-    stats = None
-    for _ in range(args.steps):
-        stats = eng.run()
-        kernel_ms.append(stats["kernel_ms"])
-    barrier()
-    elapsed = time.perf_counter() - t0
-
-    # a checksum of the per-system state digests (sums of their 32-bit
-    # halves: order-free, so identical for any GPU count), read back after the timed region
-    dg = eng.read_results()[0]
-    dsum = digest_sum(dg)
-    elapsed, totals = reduce_totals(
-        elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
-                                  stats["dropped"]] + dsum, torch.device("cuda", dev), world)
-
+    sys_base, M = shard(rank, world, args.systems)
+    elapsed, totals, stats, kernel_ms = run_kind(dash, args, args.kind, M, sys_base, world, dev,
+                                                 args.steps, tier_flag)
     instr_per_step = world * M * 8 * args.len
     value = instr_per_step * args.steps / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    achieved = M * 8 * args.len * BYTES_PER_INSTR / avg_kernel_s
+    full = M == 1 << 20 and args.len == 4096 and args.cache_size == 4
+    prof = read_profile(args.kind) if full else None
 
-    prof = read_profile(args.kind) if (M == 1 << 20 and args.len == 4096 and args.cache_size == 4) else None
+    # configs[3] beside the headline: its own warmup and timed steps (same barriers)
+    cont = None
+    if args.contention_steps > 0 and args.kind == "uniform":
+        c_el, c_tot, c_stats, c_kms = run_kind(dash, args, "contention", M, sys_base, world, dev,
+                                               args.contention_steps, tier_flag)
+        c_prof = read_profile("contention") if full else None
+        c_avg = sum(c_kms) / len(c_kms) / 1e3
+        cont = {"workload": f"{M} systems/GPU x 8 nodes x {args.len} contention RD/WR per node (90 % WR to "
+                            f"0x00-0x03), CACHE_SIZE={args.cache_size} (BASELINE configs[3])",
+                "value": instr_per_step * args.contention_steps / c_el, "unit": "instr/s",
+                "steps": args.contention_steps, "warmup": args.warmup,
+                "ms_per_step": c_el / args.contention_steps * 1e3,
+                "kernel_ms_avg": c_avg * 1e3, "kernel_ms_steps": [round(x, 3) for x in c_kms],
+                "roofline": roofline(M, args, c_avg, c_prof),
+                "valu_issue": valu_issue(c_prof, c_stats["wave_rounds"]),
+                "tier_systems": c_stats["tier_systems"], "wave_rounds": c_stats["wave_rounds"],
+                "totals": totals_dict(c_tot)}
+
     if rank == 0:
-        cpu = None
+        cpu, port, note = None, None, None
         if world == 1 and not args.no_cpu_baseline:
+            kind_id = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
+                       "locality": dash.GEN_LOCALITY}[args.kind]
+            locality = int(round(args.locality * 65536)) if args.kind == "locality" else 0
             if args.cpu_kind == "reference":
                 if args.cache_size != 4 or args.kind == "locality":
-                    raise SystemExit("the reference baseline binary is built for CACHE_SIZE 4, uniform/contention")
-                cpu = ref_baseline(args, args.seed, kind, args.cpu_seconds)
-            else:
-                cpu = cpu_baseline(args, args.seed, kind, locality, args.cpu_seconds)
+                    note = "the reference baseline binary is built for CACHE_SIZE 4, uniform/contention traces"
+                else:
+                    try:
+                        cpu = ref_baseline(args, args.seed, kind_id, args.cpu_seconds)
+                    except Exception as e:  # reported, never substituted by the port
+                        note = f"reference baseline unavailable: {e}"
+            port = cpu_baseline(args, args.seed, kind_id, locality, args.cpu_seconds)
+            if args.cpu_kind == "port":
+                cpu, port = port, None
         line = {
             "metric": "simulated instr/sec (whole node), 8-core DASH systems; % HBM roofline",
             "value": value,
@@ -434,7 +623,12 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": None,
+            # BASELINE.md publishes no number: the ratio is against cpu_baseline measured in this run
+            "vs_baseline": value / cpu["value"] if cpu else None,
+            "vs_baseline_basis": (f"value / cpu_baseline.value ({cpu['kind']}"
+                                  + (f", mode {cpu['mode']}" if cpu.get("mode") else "")
+                                  + ", measured on this box's host in this run; BASELINE.md publishes no number)")
+            if cpu else None,
             "dtype": "u8",
             "data": "synthetic (on-device counter-based generator, seed keyed by global system id)",
             "config": {"workload": f"{M} systems/GPU x 8 nodes x {args.len} {args.kind} RD/WR per node, "
@@ -442,34 +636,22 @@ def main():
                        "systems_per_gpu": M, "num_procs": 8, "instr_per_node": args.len,
                        "cache_size": args.cache_size, "trace": args.kind,
                        "parallelism": f"systems sharded over {world} GPU(s)"},
-            "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9,
-                         "unit": "GB/s", "frac": achieved / PEAK_HBM,
-                         "traffic": prof.get("hbm_bytes_per_launch") if prof else None},
-            # the bound that actually binds this integer state machine: VALU issue,
-            # one wave-instruction per cycle per CU
-            # VALU issue rate of the first-tier launch, from its own PMC run (count / duration)
-            "valu_issue": ({"achieved": prof["valu_per_launch"] / (prof["kernel_ms"] / 1e3),
-                            "peak": VALU_PEAK, "unit": "wave-instr/s",
-                            "frac": prof["valu_per_launch"] / (prof["kernel_ms"] / 1e3) / VALU_PEAK,
-                            "frac_of_simd32_issue": prof["valu_per_launch"] / (prof["kernel_ms"] / 1e3)
-                            / VALU_PEAK_SIMD32,
-                            "valu_per_wave_round": prof["valu_per_launch"] / max(stats["wave_rounds"], 1),
-                            "salu_per_wave_round": prof.get("sq_insts_salu", 0.0) / max(stats["wave_rounds"], 1),
-                            "lds_bank_conflict_frac": (prof["sq_lds_bank_conflict"] / prof["sq_lds_idx_active"]
-                                                       if prof.get("sq_lds_idx_active") else None),
-                            "l2_hit_rate": prof.get("l2_hit_rate"),
-                            "source": prof.get("source")} if prof else None),
+            "roofline": roofline(M, args, avg_kernel_s, prof),
+            # what binds this integer state machine: instruction issue
+            "valu_issue": valu_issue(prof, stats["wave_rounds"]),
             "cpu_baseline": cpu,
+            "cpu_baseline_note": note,
+            "cpu_port": port,
             "kernel_ms_avg": avg_kernel_s * 1e3,
             "kernel_ms_steps": [round(x, 3) for x in kernel_ms],
             "tier_systems": stats["tier_systems"],
             "wave_rounds": stats["wave_rounds"],
-            "totals": {"hist": totals[:13], "instructions_per_step": totals[13],
-                       "rounds_total": totals[14], "err_systems": totals[15], "dropped": totals[16],
-                       "digest_sum": totals[17:19]},
+            # systems whose run hit the reference's undefined send to node 15 (ref :772,786):
+            # parity there is with the engine's defined drop-and-flag rule
+            "totals": totals_dict(totals),
+            "contention": cont,
         }
         print(json.dumps(line), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

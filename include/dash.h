@@ -59,6 +59,9 @@ extern "C" {
 #define DASH_ERR_CTZ0 4u      /* ctz(0) on an EM entry: dropped (ref :209,451) */
 #define DASH_ERR_DEADLOCK 8u  /* quiescent with a node still waiting */
 #define DASH_ERR_ROUNDCAP 16u /* stopped at max_rounds */
+#define DASH_ERR_STUCK 32u    /* a receiver queue reached MSG_BUFFER_SIZE (256): head == tail, so the
+                                 reference never drains it again (:167-170); its messages stay
+                                 unhandled and later sends to it drop (:754-761). Modelled exactly. */
 
 /* transactionType ordinals (ref :30-44) */
 enum dash_txn {
@@ -142,12 +145,18 @@ typedef struct dash_ctx dash_t;
 /* ---- lifecycle / device path (libdash.so, HIP) ---- */
 int dash_create(const dash_cfg *cfg, dash_t **out);
 void dash_destroy(dash_t *h);
+/* the handle's last error message; dash_last_error(NULL) = the message of the last failed
+   handle-less call (dash_create, dash_run_host_batched) on the calling thread. The library
+   never writes to stderr. */
 const char *dash_last_error(const dash_t *h);
 
 /* traces: packed u16 (bit15 = WR, bits 14..8 = address, bits 7..0 = value),
    layout [sys][node][stride]; lens[sys*num_procs + node]. Synchronous: the caller's
    buffer is read (for power-of-two num_procs, by one strided H2D copy) before return;
-   words at or past a node's length are never simulated. */
+   words at or past a node's length are never simulated. An RD word's value bits are
+   ignored: the reference parses every RD with value 0 (:839) and later fills REPLY_ID /
+   REPLY_WR / FLUSH_INVACK lines with the last issued value (:383,470,531), so the library
+   clears them on the device after the copy (one pass over the trace buffer). */
 int dash_load_traces(dash_t *h, const uint16_t *packed, uint64_t stride, const uint32_t *lens,
                      uint64_t num_systems);
 /* Host-buffer throughput path (replaces the same load+run for callers whose traces sit in
@@ -155,7 +164,9 @@ int dash_load_traces(dash_t *h, const uint16_t *packed, uint64_t stride, const u
    on two handles made from *cfg (num_systems = the batch size), each driven by its own host
    thread and HIP stream, so one batch's H2D copy overlaps another's run. Results equal one
    dash_load_traces + dash_run over all systems: merged *stats (kernel_ms = sum over
-   batches), and per-system digests / rounds / errors into the optional arrays. */
+   batches), and per-system digests / rounds / errors into the optional arrays. The handles
+   are made without DASH_KEEP_STATE and event logs (nothing here returns them); the first
+   failing batch stops both threads, and dash_last_error(NULL) then holds its message. */
 int dash_run_host_batched(const dash_cfg *cfg, const uint16_t *packed, uint64_t stride,
                           const uint32_t *lens, uint64_t num_systems, uint32_t batches,
                           dash_stats *stats, uint64_t *digests, uint32_t *rounds, uint32_t *errors);

@@ -326,7 +326,9 @@ static void issue_instruction(osys *sy, int tid) {
     uint16_t w = nd->trace[nd->idx++];
     uint8_t type = (w & 0x8000) ? 'W' : 'R';
     uint8_t address = (uint8_t)((w >> 8) & 0x7F);
-    uint8_t value = (uint8_t)(w & 0xFF);
+    /* initializeProcessor parses every RD with value 0 (ref :839), whatever the packed word's
+       bits 7..0 hold; the value is used later by REPLY_ID/REPLY_WR/FLUSH_INVACK (:383,470,531) */
+    uint8_t value = type == 'W' ? (uint8_t)(w & 0xFF) : 0;
     nd->instr_type = type;
     nd->instr_address = address;
     nd->instr_value = value;
@@ -454,7 +456,10 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
         int active = 0;
         for (int t = 0; t < N; t++) {
             onode *nd = &sy->node[t];
-            if (nd->qcount > 0 || (!nd->waiting && nd->idx < nd->count)) active = 1;
+            /* a full queue (qcount == capacity) has head == tail: the reference's drain loop
+               (ref :167-170) never pops it again */
+            if ((nd->qcount > 0 && nd->qcount < (uint32_t)sy->ring) || (!nd->waiting && nd->idx < nd->count))
+                active = 1;
         }
         if (!active) break;
         if (cfg->max_rounds && out->rounds >= cfg->max_rounds) {
@@ -468,7 +473,7 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
             onode *nd = &sy->node[t];
             nd->nout = 0;
             if (cfg->arb_seed && orc_arb_stall(cfg->arb_seed, out->rounds - 1, (uint32_t)t)) continue;
-            if (nd->qcount > 0) {
+            if (nd->qcount > 0 && nd->qcount < (uint32_t)sy->ring) {
                 omsg m = nd->q[nd->head];
                 nd->head = (nd->head + 1) % (uint32_t)sy->ring;
                 nd->qcount--;
@@ -502,7 +507,7 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
                 onode *dst = &sy->node[rcv];
                 if (dst->qcount < (uint32_t)sy->ring) {
                     dst->q[(dst->head + dst->qcount) % (uint32_t)sy->ring] = src->out[k];
-                    dst->qcount++;
+                    if (++dst->qcount == (uint32_t)sy->ring) out->errors |= ORC_ERR_STUCK;
                 } else {
                     out->errors |= ORC_ERR_OVERFLOW;
                     out->dropped++;

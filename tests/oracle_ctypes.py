@@ -22,6 +22,7 @@ MAX_PROCS = 8
 MEM = 16
 MAX_CACHE = 16
 NTXN = 13
+ERR_OVERFLOW, ERR_OOB, ERR_CTZ0, ERR_DEADLOCK, ERR_ROUNDCAP, ERR_STUCK = 1, 2, 4, 8, 16, 32
 TXN_NAMES = ["READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID", "INV",
              "UPGRADE", "WRITEBACK_INV", "WRITEBACK_INT", "FLUSH", "FLUSH_INVACK",
              "EVICT_SHARED", "EVICT_MODIFIED"]

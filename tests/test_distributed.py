@@ -54,3 +54,34 @@ def test_two_rank_shards_reduce_to_single_run():
         assert totals == expect
     digests = res[0][2] + res[1][2]
     assert digests == single["digests"].tolist()  # results independent of the GPU count
+
+
+def _bench(*argv, env=None, timeout=180):
+    import json
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parent.parent
+    e = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    e.update(env or {})
+    r = subprocess.run([sys.executable, str(root / "bench.py"), *argv], capture_output=True, text=True,
+                       timeout=timeout, env=e, cwd=root)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus N` without torchrun starts N ranks itself (the driver's 1/2/4/8-GPU
+    lines come from this same command form); each global system lands on exactly one rank."""
+    r, d = _bench("--gpus", "2", "--dist-selftest", "--systems", "1000")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert d == {"world": 2, "systems_owned": 2000, "each_once": True, "local_rank": 0}
+    r, d = _bench("--gpus", "4", "--dist-selftest", "--systems", "5")
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert d["world"] == 4 and d["systems_owned"] == 20 and d["each_once"]
+
+
+def test_bench_rejects_world_size_mismatch():
+    r, d = _bench("--gpus", "1", "--dist-selftest", env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode != 0 and d is None
+    assert "must equal --gpus" in r.stderr

@@ -15,6 +15,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 ARGS = ["--systems", "2048", "--len", "512", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+# the torchrun rehearsal keeps the headline workload only
 
 
 def _free_port():
@@ -33,12 +34,12 @@ def test_two_ranks_match_one_process():
     env = dict(os.environ)
     two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-                          str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo"] + ARGS,
+                          str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--contention-steps", "0"] + ARGS,
                          capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert two.returncode == 0, two.stderr[-3000:]
     d2 = _line(two.stdout)
-    one = subprocess.run([sys.executable, str(ROOT / "bench.py")] + ARGS[:1] + ["4096"] + ARGS[2:],
-                         capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    one = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--contention-steps", "0"] + ARGS[:1] + ["4096"]
+                         + ARGS[2:], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert one.returncode == 0, one.stderr[-3000:]
     d1 = _line(one.stdout)
     assert d2["n_gpus"] == 2 and d2["scaling"] == "weak"
@@ -49,3 +50,21 @@ def test_two_ranks_match_one_process():
     assert d2["totals"]["digest_sum"] == d1["totals"]["digest_sum"]  # final states, order-free
     # value = all ranks' instructions / max-over-ranks time
     assert abs(d2["value"] - 4096 * 8 * 512 / (d2["ms_per_step"] / 1e3)) < 1e-6 * d2["value"]
+
+
+def test_bench_spawns_two_ranks_without_torchrun():
+    """`bench.py --gpus 2` starts its own two ranks (no torchrun): same totals as one process."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    two = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                          "--contention-steps", "1"] + ARGS,
+                         capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert two.returncode == 0, two.stderr[-3000:]
+    d2 = _line(two.stdout)
+    one = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--contention-steps", "1"] + ARGS[:1] + ["4096"]
+                         + ARGS[2:], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = _line(one.stdout)
+    assert d2["n_gpus"] == 2 and d1["n_gpus"] == 1
+    assert d2["totals"] == d1["totals"]
+    assert d2["contention"]["totals"] == d1["contention"]["totals"]
+    assert d2["contention"]["totals"]["instructions_per_step"] == 4096 * 8 * 512

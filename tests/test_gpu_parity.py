@@ -418,3 +418,43 @@ def test_non_power_of_two_cache_size(dash, N, CS):
     check_batch(dash, packed, lens, N, CS)
     packed, lens = random_batch(rng, 48, N, 48, block_span=6, hot_frac=0.4)
     check_batch(dash, packed, lens, N, CS)
+
+
+@pytest.mark.parametrize("N", [8, 5])
+def test_rd_value_bits_ignored_at_the_boundary(dash, N):
+    """The reference parses every RD with value 0 (ref :839) and later fills REPLY_ID /
+    REPLY_WR / FLUSH_INVACK lines with the last issued value (:383,470,531): RD words
+    whose bits 7..0 are set must give the results of the clean words (dash.h contract).
+    N=8 takes the strided-copy path, N=5 the host re-layout."""
+    rng = np.random.default_rng(77 + N)
+    clean, lens = random_batch(rng, 96, N, 256, block_span=4)
+    dirty = clean.copy()
+    rd = (dirty & 0x8000) == 0
+    dirty[rd] |= rng.integers(1, 256, size=int(rd.sum())).astype(np.uint16)
+    assert (dirty != clean).any()
+    with dash.Engine(96, num_procs=N, cache_size=2, max_instr=256, keep_state=True) as eng:
+        eng.load_traces(dirty, lens)
+        stats = eng.run()
+        dig, rnd, err = eng.read_results()
+        for s in range(96):
+            res = run_system(clean[s], lens[s], num_procs=N, cache_size=2, ring_depth=256)
+            assert int(dig[s]) == res.digest and int(rnd[s]) == res.rounds and int(err[s]) == res.errors, s
+            assert state_arrays(eng.read_state(s), N, 2) == state_arrays(res.node, N, 2), s
+    assert stats["instructions"] == int(lens.sum())
+
+
+def test_full_queue_is_stuck_like_the_reference(dash):
+    """An adversarial 8-node trace (tests/golden/stuck_queue.npy, found by hill-climbing
+    queue depth on the oracle) fills a receiver queue to MSG_BUFFER_SIZE = 256. The
+    reference then has head == tail and never drains that queue again (:167-170) while
+    later sends to it drop (:754-761); the engine models exactly that at its final tier
+    (DASH_ERR_STUCK), bit-exact with the oracle."""
+    tr = np.load(GOLDEN / ".." / "stuck_queue.npy")
+    packed = tr[None, :, :].astype(np.uint16)
+    lens = np.full((1, 8), tr.shape[1], dtype=np.uint32)
+    # (max_rounds = the default cap, passed explicitly: nodes left waiting never finish their traces)
+    stats = check_batch(dash, packed, lens, 8, 1, max_rounds=1024 + 256 * tr.shape[1])
+    res = run_system(tr, lens[0], num_procs=8, cache_size=1, ring_depth=256)
+    assert res.errors & oracle_ctypes.ERR_STUCK and res.max_depth == 256
+    assert stats["err_bits"] & dash.ERR_STUCK
+    assert stats["tier_systems"][2] == 1  # handed from the 16- and 32-deep tiers to the reference depth

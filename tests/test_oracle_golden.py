@@ -8,6 +8,8 @@ lockstep-ascending values (they are schedule-dependent, App. C).
 """
 import collections
 
+import numpy as np
+
 import pytest
 
 from oracle_ctypes import GOLDEN, dump_node, load_test_dir, run_system
@@ -79,3 +81,39 @@ def test_dump_byte_size():
     tr, lens = load_test_dir(GOLDEN / "sample")
     res = run_system(tr, lens)
     assert len(dump_node(res, 0).encode()) == 1955
+
+
+def test_rd_value_bits_are_ignored():
+    """initializeProcessor stores value 0 for every RD (ref :839): the packed word's bits
+    7..0 of an RD never reach the state (REPLY_ID/REPLY_WR/FLUSH_INVACK fill with the last
+    issued value, :383,470,531)."""
+    import oracle_ctypes as oc
+    rng = np.random.default_rng(5)
+    for _ in range(40):
+        N, L = 8, 96
+        w = rng.random((N, L)) < 0.5
+        node = rng.integers(0, N, (N, L))
+        blk = rng.integers(0, 4, (N, L))
+        val = rng.integers(0, 256, (N, L))
+        clean = ((w << 15) | (((node << 4) | blk) << 8) | np.where(w, val, 0)).astype(np.uint16)
+        dirty = np.where(w, clean, clean | rng.integers(1, 256, (N, L))).astype(np.uint16)
+        lens = np.full(N, L, np.uint32)
+        a = oc.run_system(clean, lens, num_procs=N, cache_size=2)
+        b = oc.run_system(dirty, lens, num_procs=N, cache_size=2)
+        assert a.digest == b.digest and a.rounds == b.rounds and list(a.hist) == list(b.hist)
+
+
+def test_stuck_queue_fixture():
+    """tests/golden/stuck_queue.npy fills one receiver queue to MSG_BUFFER_SIZE (256): the
+    reference's drain loop needs head != tail (:167-170), so that queue is never popped
+    again and later sends to it drop (:754-761). The oracle models exactly that."""
+    import oracle_ctypes as oc
+    tr = np.load(oc.GOLDEN.parent / "stuck_queue.npy")
+    lens = np.full(8, tr.shape[1], np.uint32)
+    r = oc.run_system(tr, lens, num_procs=8, cache_size=1, ring_depth=256)
+    assert r.max_depth == 256
+    assert r.errors & oc.ERR_STUCK and r.errors & oc.ERR_OVERFLOW
+    assert r.errors & oc.ERR_DEADLOCK  # a node waits on a reply parked in the stuck queue
+    # pinned: the run that found the fixture (tests/golden/make_stuck_queue.py); the nodes
+    # left waiting on replies parked in the stuck queue never finish their traces
+    assert (r.rounds, r.digest, r.dropped, r.instructions) == (34616, 4822832980353165774, 4, 24369)

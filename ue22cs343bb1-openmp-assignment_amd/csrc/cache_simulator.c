@@ -211,7 +211,8 @@ int main(int argc, char *argv[]) {
     int rc = (dbg_instr || dbg_msg) ? simulate_traced(dir, n, cs, m, out, dev, dbg_instr, dbg_msg, &st)
                                     : dash_simulate_dir(dir, n, cs, m, out, dev, &st);
     if (rc != DASH_OK) {
-        fprintf(stderr, "cache_simulator: failed (%d)\n", rc);
+        const char *why = dash_last_error(NULL);
+        fprintf(stderr, "cache_simulator: %s (%d)\n", why[0] ? why : "failed", rc);
         return EXIT_FAILURE;
     }
     if (show) print_stats(&st);

@@ -89,7 +89,12 @@ static hipError_t reset_hint(dash_t* h) {
 
 extern "C" {
 
-const char* dash_last_error(const dash_t* h) { return h ? h->msg : "null handle"; }
+// message of the last failed handle-less call (dash_create, dash_run_host_batched) on this thread
+static thread_local char g_msg[256] = "";
+
+static void set_global_msg(const char* m) { snprintf(g_msg, sizeof g_msg, "%s", m ? m : ""); }
+
+const char* dash_last_error(const dash_t* h) { return h ? h->msg : g_msg; }
 
 void* dash_stream(dash_t* h) { return h ? (void*)h->stream : nullptr; }
 
@@ -197,7 +202,7 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
         chk(hipMalloc(&h->d_state, std::max<uint64_t>(nsys * N, 1) * (16 + CS) * sizeof(uint32_t)),
             "hipMalloc(state)");
     if (rc != DASH_OK) {
-        fprintf(stderr, "dash_create: %s\n", h->msg);
+        set_global_msg(h->msg);  // no stderr from the library: dash_last_error(NULL) has it
         dash_destroy(h);
         return rc;
     }
@@ -249,6 +254,8 @@ int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const u
             HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 8, hipMemcpyHostToDevice, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));  // `host` is pageable and local
     }
+    // RD carries value 0 whatever the caller's bits 7..0 say (ref :839; dash.h)
+    HIPCHK(h, dash::launch_clear_rd(h->d_trace, words, h->stream));
     if (num_systems)
         HIPCHK(h, hipMemcpyAsync(h->d_lens, lens, num_systems * N * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, reset_hint(h));
@@ -605,7 +612,7 @@ int dash_simulate_dir(const char* dir, uint32_t num_procs, uint32_t cache_size, 
     if (rc != DASH_OK) return rc;
     rc = dash_load_dir(h, dir, 0);
     if (rc != DASH_OK) {
-        fprintf(stderr, "%s\n", h->msg);
+        set_global_msg(h->msg);
         dash_destroy(h);
         return rc;
     }
@@ -617,7 +624,7 @@ int dash_simulate_dir(const char* dir, uint32_t num_procs, uint32_t cache_size, 
         snprintf(path, sizeof path, "%s/core_%u_output.txt", out_dir ? out_dir : ".", t);
         rc = dash_dump_file(&st[t], t, cache_size, path);
     }
-    if (rc != DASH_OK && h->msg[0]) fprintf(stderr, "%s\n", h->msg);
+    if (rc != DASH_OK) set_global_msg(h->msg);
     dash_destroy(h);
     return rc;
 }
@@ -634,16 +641,22 @@ extern "C" int dash_run_host_batched(const dash_cfg* cfg, const uint16_t* packed
     const uint64_t nb = num_systems / batches, N = cfg->num_procs;
     dash_cfg c = *cfg;
     c.num_systems = nb;
+    // throughput path: per-system state snapshots and event logs are not returned here,
+    // so the handles do not allocate them
+    c.flags &= ~(uint32_t)DASH_KEEP_STATE;
+    c.trace_events = 0;
     const unsigned nh = batches < 2 ? 1u : 2u;
     dash_t* h[2] = {nullptr, nullptr};
+    set_global_msg("");
     int rc = DASH_OK;
     for (unsigned i = 0; i < nh && rc == DASH_OK; i++) rc = dash_create(&c, &h[i]);
     dash_stats part[2];
     memset(part, 0, sizeof part);
     int trc[2] = {DASH_OK, DASH_OK};
+    std::atomic<bool> stop{false};  // the first failing lane stops the other one too
     // handle i (its own HIP stream) takes batches i, i+2, ...: while one copies, the other runs
     auto lane = [&](unsigned i) {
-        for (uint64_t b = i; b < batches && trc[i] == DASH_OK; b += nh) {
+        for (uint64_t b = i; b < batches && !stop.load(); b += nh) {
             int r = dash_load_traces(h[i], packed + b * nb * N * stride, stride, lens + b * nb * N, nb);
             dash_stats st;
             if (r == DASH_OK) r = dash_run(h[i], &st);
@@ -652,6 +665,7 @@ extern "C" int dash_run_host_batched(const dash_cfg* cfg, const uint16_t* packed
                                       rounds ? rounds + b * nb : nullptr, errors ? errors + b * nb : nullptr);
             if (r != DASH_OK) {
                 trc[i] = r;
+                stop.store(true);
                 break;
             }
             dash_stats& p = part[i];
@@ -674,6 +688,7 @@ extern "C" int dash_run_host_batched(const dash_cfg* cfg, const uint16_t* packed
         for (unsigned i = 0; i < nh; i++) pool.emplace_back(lane, i);
         for (auto& t : pool) t.join();
         rc = trc[0] != DASH_OK ? trc[0] : trc[1];
+        if (rc != DASH_OK) set_global_msg(h[trc[0] != DASH_OK ? 0 : 1]->msg);
     }
     for (unsigned i = 0; i < nh; i++)
         if (h[i]) dash_destroy(h[i]);

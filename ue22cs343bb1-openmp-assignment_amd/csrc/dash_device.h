@@ -11,6 +11,7 @@ constexpr uint32_t DASH_ERR_OOB_D = 2u;
 constexpr uint32_t DASH_ERR_CTZ0_D = 4u;
 constexpr uint32_t DASH_ERR_DEADLOCK_D = 8u;
 constexpr uint32_t DASH_ERR_ROUNDCAP_D = 16u;
+constexpr uint32_t DASH_ERR_STUCK_D = 32u;
 
 // device statistics block (u64 words)
 enum : uint32_t {
@@ -80,6 +81,8 @@ constexpr uint32_t RING_TIERS[NUM_TIERS] = {16, 32, 256};
 constexpr uint32_t CHUNK_INSTR = 4;  // instructions per 8-B trace chunk
 hipError_t launch_gen(const GenArgs& g, hipStream_t s);
 // skip[list[i]] = 1 for i < n
+// RD words carry value 0 (ref :839): clears bits 7..0 of every word whose bit 15 is 0
+hipError_t launch_clear_rd(uint2* trace, uint64_t words, hipStream_t s);
 hipError_t launch_mark(const uint32_t* list, uint64_t n, uint8_t* skip, hipStream_t s);
 
 }  // namespace dash

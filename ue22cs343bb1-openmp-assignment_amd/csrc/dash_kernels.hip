@@ -213,7 +213,9 @@ void sim_kernel(const SimArgs a) {
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
         const bool waiting = __builtin_amdgcn_inverse_ballot_w64(wmask);
         bool can_issue = !waiting & (pc < lenx);
-        bool nonempty = cq != 0;
+        // the final (reference-depth) tier: a queue that reached MSG_BUFFER_SIZE has
+        // head == tail, so the reference's drain loop (ref :167-170) never pops it again
+        bool nonempty = FINAL ? (cq != 0) & (cq != RING * SLOT) : cq != 0;
         bool active = nonempty | can_issue;
         if (r == cap) {  // wave-uniform: every system still active has run `cap` rounds
             COLD();
@@ -283,7 +285,7 @@ void sim_kernel(const SimArgs a) {
         const uint32_t ins = *reinterpret_cast<const uint16_t*>(ldsb + L::WND * 4 + (pc & (WIN * WCHUNK * PCU - 1)) + sw * 2);
         const bool do_issue = !nonempty & can_issue & !stall;
         pc += do_issue ? PCU : 0u;
-        if constexpr (ARB)
+        if constexpr (ARB || FINAL)
             cq -= has_msg ? SLOT : 0u;
         else
             cq = __builtin_elementwise_sub_sat(cq, SLOT);  // pop (cq is a multiple of SLOT)
@@ -486,6 +488,12 @@ void sim_kernel(const SimArgs a) {
         if constexpr (FINAL) n = min(n, RING * SLOT - cq);  // sendMessage's drop (ref :754-761)
         tq = (tq + n) & RMASK;
         cq += n;
+        if constexpr (FINAL) {
+            if (cq == RING * SLOT) {  // full: stuck for good (DASH_ERR_STUCK)
+                COLD();
+                err |= DASH_ERR_STUCK_D;
+            }
+        }
         maxd = max(maxd, cq);
     }
 
@@ -681,6 +689,24 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring
     case 8: return launch_sim_p<8>(a, cs, ring, groups, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+__global__ __launch_bounds__(256) void clear_rd_kernel(uint2* trace, uint64_t words) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint2 v = trace[i];
+        // per 16-bit half: keep bits 7..0 only when bit 15 (WR) is set
+        v.x &= (((v.x >> 15) & 0x00010001u) * 0xFFu) | 0xFF00FF00u;
+        v.y &= (((v.y >> 15) & 0x00010001u) * 0xFFu) | 0xFF00FF00u;
+        trace[i] = v;
+    }
+}
+
+hipError_t launch_clear_rd(uint2* trace, uint64_t words, hipStream_t s) {
+    if (words == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((words + 255) / 256, 256ull * 64);  // grid-stride
+    hipLaunchKernelGGL(clear_rd_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, trace, words);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void mark_kernel(const uint32_t* list, uint64_t n, uint8_t* skip) {

@@ -39,7 +39,7 @@ TXN_NAMES = ("READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID"
 
 OK, EINVAL, EIO, EPARSE, EADDR, EDEVICE, ENOMEM, ESTATE, ETRUNC = 0, -1, -2, -3, -4, -5, -6, -7, -8
 EV_MSG, EV_INSTR = 0, 1
-ERR_OVERFLOW, ERR_OOB, ERR_CTZ0, ERR_DEADLOCK, ERR_ROUNDCAP = 1, 2, 4, 8, 16
+ERR_OVERFLOW, ERR_OOB, ERR_CTZ0, ERR_DEADLOCK, ERR_ROUNDCAP, ERR_STUCK = 1, 2, 4, 8, 16, 32
 KEEP_STATE = 1
 TIER_FROM_32, TIER_FROM_256 = 2, 4
 NUM_TIERS = 3
@@ -155,10 +155,14 @@ def lib() -> ctypes.CDLL:
     return L
 
 
+# handle-less entry points whose failure text dash_last_error(NULL) holds (dash.h)
+_GLOBAL_MSG = ("dash_create", "dash_run_host_batched", "dash_simulate_dir")
+
+
 def _check(rc: int, what: str, handle=None):
     if rc != OK:
         msg = what
-        if handle:
+        if handle or what in _GLOBAL_MSG:
             detail = lib().dash_last_error(handle)
             if detail:
                 msg = f"{what}: {detail.decode(errors='replace')}"

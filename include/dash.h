@@ -82,7 +82,8 @@ typedef struct dash_cfg {
     uint32_t max_instr;   /* longest trace per node (ref MAX_INSTR_NUM 32, :10) */
     uint32_t flags;       /* DASH_KEEP_STATE */
     uint64_t num_systems; /* independent systems in the batch */
-    uint64_t max_rounds;  /* per-system round cap; 0 = 1024 + 256*max_instr */
+    uint64_t max_rounds;  /* per-system round cap (engine-defined: the reference never exits),
+                             rounded up to a multiple of 4; 0 = 1024 + 256*max_instr */
     int32_t device;       /* HIP device ordinal */
     uint32_t trace_events; /* per-node event log capacity for DEBUG_MSG / DEBUG_INSTR
                               emission (ref :179-182, :649-652); 0 = no log */

@@ -204,6 +204,7 @@ def test_round_cap(dash):
     rng = np.random.default_rng(11)
     packed, lens = random_batch(rng, 40, 4, 32, fixed_len=True)
     check_batch(dash, packed, lens, 4, 4, max_rounds=20)
+    check_batch(dash, packed, lens, 4, 4, max_rounds=21)  # rounded up to 24 by both
 
 
 @pytest.mark.parametrize("kind,loc", [(0, 0), (1, 0), (2, 49152), (2, 0), (2, 65536)])

@@ -144,7 +144,9 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     if (!h) return DASH_ENOMEM;
     h->cfg = *cfg;
     if (h->cfg.max_rounds == 0) h->cfg.max_rounds = 1024ull + 256ull * cfg->max_instr;
-    if (h->cfg.max_rounds > 0xFFFFFFFFull) h->cfg.max_rounds = 0xFFFFFFFFull;
+    // checked at the first round of every WCHUNK-round trip of the kernel: a multiple of 4
+    h->cfg.max_rounds = (h->cfg.max_rounds + 3) & ~3ull;
+    if (h->cfg.max_rounds > 0xFFFFFFFCull) h->cfg.max_rounds = 0xFFFFFFFCull;
     h->seg = next_pow2(N);
     const uint64_t spw = 64 / h->seg;
     h->groups = (cfg->num_systems + spw - 1) / spw;

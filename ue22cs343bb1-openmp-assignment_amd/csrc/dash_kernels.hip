@@ -100,15 +100,21 @@ struct Lds {  // 32-bit word offsets
 __device__ __forceinline__ void chunk_words(uint2 v, uint32_t& x, uint32_t& y) { x = v.x; y = v.y; }
 __device__ __forceinline__ void chunk_words(uint32_t v, uint32_t& x, uint32_t& y) { x = v; y = 0; }
 
-// wave-wide vote without HIP's int round trip (bool -> 0/1 -> compare)
+// wave-wide lane masks: M() makes one from a per-lane condition (the compare's own SGPR
+// result), B() reads a lane's bit back as the condition of a select or branch
+using mask_t = uint64_t;
+__device__ __forceinline__ mask_t M(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+__device__ __forceinline__ bool B(mask_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 __device__ __forceinline__ uint64_t vote(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 // keeps a rarely taken branch a branch (no if-conversion onto the common path)
 #define COLD() asm volatile("" ::: "memory")
 
-// ARB: seeded legal schedule -- per round, a node sits out with
-// probability 1/4 and senders deliver in a seeded affine order (oracle twins:
-// orc_arb_stall, orc_arb_prio); otherwise every node steps, lowest sender first
-template <int P, int CS, uint32_t RING, bool ARB>
+// SLOW: the kernel for the rarely used run options, checked at run time: a seeded legal
+// schedule (a.arb_seed != 0, DESIGN.md §2 -- per round, a node sits out with probability
+// 1/4 and senders deliver in a seeded affine order; oracle twins orc_arb_stall,
+// orc_arb_prio) and the DEBUG_MSG / DEBUG_INSTR event log (a.events). The fast kernel
+// (SLOW = false) has neither: every node steps, lowest sender first.
+template <int P, int CS, uint32_t RING, bool SLOW>
 __global__ __launch_bounds__(64)
 #if DASH_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(DASH_WAVES_PER_EU)))
@@ -202,36 +208,41 @@ void sim_kernel(const SimArgs a) {
     const uint32_t wES = T_ES | (t << 4), wEM = T_EMOD | (t << 4);  // eviction notice, sender part
 
     uint32_t r = 0;
+    const uint32_t sw2 = sw * 2u;  // byte offset of this lane's u16 in a 128-B row
     // WCHUNK rounds per trip, unrolled: the housekeeping point (refill, quiescence vote,
     // overflow stop) is the first round of every trip, a compile-time position
     static_assert(DASH_QCHECK == WCHUNK, "one housekeeping point per WCHUNK rounds");
     for (bool done = false; !done;)
 #pragma unroll
     for (uint32_t k = 0; k < WCHUNK; ++k, ++r) {
+        // Every predicate below is a wave-wide lane mask (an SGPR pair): one compare makes
+        // it, the scalar unit combines them, v_cndmask consumes them. The kernel is bound by
+        // VALU issue, so no predicate is ever materialised in a VGPR.
         // ---- quiescence / round cap, on start-of-round state ----
         // A system is active while any of its nodes has a message or can issue;
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
-        const bool waiting = __builtin_amdgcn_inverse_ballot_w64(wmask);
-        bool can_issue = !waiting & (pc < lenx);
+        mask_t mIss = M(pc < lenx) & ~wmask;  // not waitingForReply (ref :624-629), instructions left
         // the final (reference-depth) tier: a queue that reached MSG_BUFFER_SIZE has
         // head == tail, so the reference's drain loop (ref :167-170) never pops it again
-        bool nonempty = FINAL ? (cq != 0) & (cq != RING * SLOT) : cq != 0;
-        bool active = nonempty | can_issue;
-        if (r == cap) {  // wave-uniform: every system still active has run `cap` rounds
+        mask_t mMsg = FINAL ? M(cq != 0) & M(cq != RING * SLOT) : M(cq != 0);
+        mask_t mAct = mMsg | mIss;
+        // the round cap is a multiple of WCHUNK (dash_create rounds it up), so it can only
+        // fall on a trip's first round
+        if (k == 0 && r == cap) {  // wave-uniform: every system still active has run `cap` rounds
             COLD();
-            const uint64_t act = vote(active);
-            const bool kill = ((uint32_t)(act >> seg) & SEGMASK) != 0;
-            wmask &= ~vote(kill);
+            const bool kill = ((uint32_t)(mAct >> seg) & SEGMASK) != 0;
+            const mask_t mKill = M(kill);
+            wmask &= ~mKill;
+            mMsg &= ~mKill;
+            mIss &= ~mKill;
+            mAct &= ~mKill;
             if (kill) {
                 err |= DASH_ERR_ROUNDCAP_D;
-                nonempty = false;
                 cq = 0;
                 lenx = pc;
-                can_issue = false;
-                active = false;
             }
         }
-        if (active) {
+        if (B(mAct)) {
             COLD();
             last_act = r;
         }
@@ -244,20 +255,22 @@ void sim_kernel(const SimArgs a) {
         if (k == 0) {
             // quiescence is absorbing, so testing it once per trip only adds idle
             // rounds (no state changes, not counted in `rounds`)
-            if (vote(active) == 0) {
+            if (mAct == 0) {
                 done = true;
                 break;
             }
             // a non-final tier stops a system soon after its first overflow: it will be
             // re-simulated from scratch at the next depth, its results here are void
             if (!FINAL) {
-                const uint64_t ovf = vote(maxd > RING * SLOT);
+                const mask_t ovf = M(maxd > RING * SLOT);
                 if (ovf != 0) {
                     COLD();
                     const bool stop = ((uint32_t)(ovf >> seg) & SEGMASK) != 0;
-                    wmask &= ~vote(stop);
+                    const mask_t mStop = M(stop);
+                    wmask &= ~mStop;
+                    mMsg &= ~mStop;
+                    mIss &= ~mStop;
                     if (stop) {
-                        nonempty = false;
                         cq = 0;
                         lenx = pc;
                     }
@@ -271,158 +284,162 @@ void sim_kernel(const SimArgs a) {
         }
 
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
-        bool stall = false;
+        mask_t mStall = 0;
         uint32_t bitI = 1u << (4 * t);
-        if constexpr (ARB) {  // round keys are wave-uniform: computed on the scalar unit
+        if (SLOW && a.arb_seed) {  // round keys are wave-uniform: computed on the scalar unit
             const uint64_t rk = a.arb_seed ^ ((uint64_t)r * 0x9E3779B97F4A7C15ull);
             const uint64_t key = fmix64(rk), skey = fmix64(rk ^ 0xD1B54A32D192ED03ull);
-            stall = ((skey >> (8 * t)) & 3u) == 0;
+            mStall = M(((skey >> (8 * t)) & 3u) == 0);
             const uint32_t A = ((uint32_t)key & (P - 1)) | 1u, Bc = (uint32_t)(key >> 8) & (P - 1);
             bitI = 1u << (4 * ((t * A + Bc) & (P - 1)));
         }
-        const bool has_msg = nonempty & !stall;
+        const mask_t mHas = mMsg & ~mStall;           // pops this round
+        const mask_t mDo = mIss & ~mMsg & ~mStall;    // issues this round
         const uint32_t m = *reinterpret_cast<const uint32_t*>(ldsb + L::RNG * 4 + ((tq - cq) & RMASK));
-        const uint32_t ins = *reinterpret_cast<const uint16_t*>(ldsb + L::WND * 4 + (pc & (WIN * WCHUNK * PCU - 1)) + sw * 2);
-        const bool do_issue = !nonempty & can_issue & !stall;
-        pc += do_issue ? PCU : 0u;
-        if constexpr (ARB || FINAL)
-            cq -= has_msg ? SLOT : 0u;
+        const uint32_t ins = *reinterpret_cast<const uint16_t*>(ldsb + L::WND * 4 + ((pc & (WIN * WCHUNK * PCU - 1)) | sw2));
+        pc += B(mDo) ? PCU : 0u;
+        if constexpr (SLOW || FINAL)
+            cq -= B(mHas) ? SLOT : 0u;
         else
             cq = __builtin_elementwise_sub_sat(cq, SLOT);  // pop (cq is a multiple of SLOT)
         // message addresses are < 0x80 (a send to a node >= N is dropped), so bits
         // 14..8 give the address of a message and of an instruction alike
-        const uint32_t mw = has_msg ? m : ins;
+        const uint32_t mw = B(mHas) ? m : ins;
         const uint32_t addr = (mw >> 8) & 0x7Fu;
         const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         // cacheIndex = blockIndex % CACHE_SIZE (ref :188)
         const uint32_t idx = CS ? b % (uint32_t)CS : (uint32_t)(a.cs_lut >> (4 * b)) & 15u;
-        // the row offsets stay in VGPRs from the loads to the stores (no recomputation)
-        uint32_t eoff = b * 64 + sw, coff = idx * 64 + sw;
+        // byte offsets of the row entries; they stay in VGPRs from the loads to the stores
+        uint32_t eoff = (b << 7) | sw2, coff = (idx << 7) | sw2;
         asm volatile("" : "+v"(eoff), "+v"(coff));
-        uint16_t* const ent = lds16 + L::ENT * 2 + eoff;
-        uint16_t* const cac = lds16 + L::CAC * 2 + coff;
+        uint16_t* const ent = reinterpret_cast<uint16_t*>(ldsb + L::ENT * 4 + eoff);
+        uint16_t* const cac = reinterpret_cast<uint16_t*>(ldsb + L::CAC * 4 + coff);
         const uint32_t e16 = *ent;
         const uint32_t c16 = *cac;
         const uint32_t mty = m & 15u;
-        if (a.events) {  // wave-uniform: the batch-of-1 trace (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652)
+        if (SLOW && a.events) {  // wave-uniform: the batch-of-1 trace (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652)
             COLD();
-            if (has_msg | do_issue) {
+            if (B(mHas | mDo)) {
                 if (nev < a.event_cap) {
                     uint32_t* e = a.events + ((sys * N + t) * a.event_cap + nev) * 2;
                     e[0] = r;
-                    e[1] = has_msg ? m : (ins | 0x80000000u);
+                    e[1] = B(mHas) ? m : (ins | 0x80000000u);
                 }
                 ++nev;
             }
         }
-        if (has_msg)  // messages handled per transactionType, per system
+        if (B(mHas))  // messages handled per transactionType, per system
             __hip_atomic_fetch_add(&lds[L::HST + mty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
 
-        // The kernel is VALU-issue bound: predicates are lane masks
-        // (one v_cmp each), combined by the scalar unit, consumed by v_cndmask.
-        const bool isW = (ins & 0x8000u) != 0;
-        const bool iR = do_issue & !isW, iW = do_issue & isW;
-        const bool RR = has_msg & (mty == T_RR), WRQ = has_msg & (mty == T_WRQ);
-        const bool RRD = has_msg & (mty == T_RRD), RWR = has_msg & (mty == T_RWR);
-        const bool RID = has_msg & (mty == T_RID), INV = has_msg & (mty == T_INV);
-        const bool UPG = has_msg & (mty == T_UPG), WBINV = has_msg & (mty == T_WBINV);
-        const bool WBINT = has_msg & (mty == T_WBINT), FLUSH = has_msg & (mty == T_FLUSH);
-        const bool FIA = has_msg & (mty == T_FIA), ES = has_msg & (mty == T_ES);
-        const bool EMOD = has_msg & (mty == T_EMOD);
+        // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
+        const mask_t mRR = mHas & M(mty == T_RR), mWRQ = mHas & M(mty == T_WRQ);
+        const mask_t mRRD = mHas & M(mty == T_RRD), mRWR = mHas & M(mty == T_RWR);
+        const mask_t mRID = mHas & M(mty == T_RID), mINV = mHas & M(mty == T_INV);
+        const mask_t mUPG = mHas & M(mty == T_UPG), mWBINV = mHas & M(mty == T_WBINV);
+        const mask_t mWBINT = mHas & M(mty == T_WBINT), mFLUSH = mHas & M(mty == T_FLUSH);
+        const mask_t mFIA = mHas & M(mty == T_FIA), mES = mHas & M(mty == T_ES);
+        const mask_t mEMOD = mHas & M(mty == T_EMOD);
+        const mask_t mIsW = M(ins >= 0x8000u);
+        const mask_t miR = mDo & ~mIsW, miW = mDo & mIsW;
 
         const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
         const uint32_t laddr = c16 & 0xFFu, lval = c16 >> 8, lst = (cst >> (2 * idx)) & 3u;
         const uint32_t msender = (m >> 4) & 7u, mval = (mw >> 16) & 0xFFu;
         const uint32_t msr = (m >> 24) & 7u;
-        const bool mds_s = (m & (1u << 27)) != 0;
         const uint32_t ival = ins & 0xFFu;
         const uint32_t sbit = 1u << msender;
 
-        // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
-        const bool dsEM = ds == D_EM, dsS = ds == D_S, dsU = !dsEM & !dsS;
-        const bool lI = lst == ST_I, lS = lst == ST_S;
-        const bool tH = t == H, tSR = t == msr;
-        const bool same = laddr == addr;
-        const bool hit = same & !lI;                     // ref :662-664
-        const bool own_hit = iW & hit & !lS;             // WR hit on M/E (:706-710)
-        const uint32_t es_bv = bv & ~sbit;               // also UPGRADE/WRITE_REQUEST's sharer list
+        const mask_t mEM = M(ds == D_EM), mS = M(ds == D_S), mU = ~(mEM | mS);
+        const mask_t mlI = M(lst == ST_I), mlS = M(lst == ST_S), mlM = M(lst == ST_M);
+        const mask_t mtH = M(t == H), mtSR = M(t == msr), mSame = M(laddr == addr);
+        const mask_t mHit = mSame & ~mlI;                 // ref :662-664
+        const mask_t mOwnHit = miW & mHit & ~mlS;         // WR hit on M/E (:706-710)
+        const uint32_t es_bv = bv & ~sbit;                // also UPGRADE/WRITE_REQUEST's sharer list
         const uint32_t es_pop = (uint32_t)__builtin_popcount(es_bv);
         const uint32_t es_own = (uint32_t)__builtin_ctz(es_bv | 0x100u);  // meaningful when es_pop == 1
-        const bool esH = ES & tH;
-        const bool es_one = esH & (es_pop == 1u);
-        const bool req = RR | WRQ;
-        const bool em_req = req & dsEM;
-        const bool ctz0 = em_req & (bv == 0u);           // ref UB (:209, :451): drop + flag
-        const bool homeH = (FLUSH | FIA) & tH;
+        const mask_t mEsH = mES & mtH;
+        const mask_t mEsOne = mEsH & M(es_pop == 1u);
+        const mask_t mReq = mRR | mWRQ;
+        const mask_t mEmReq = mReq & mEM;
+        const mask_t mCtz0 = mEmReq & M(bv == 0u);        // ref UB (:209, :451): drop + flag
+        const mask_t mHomeH = (mFLUSH | mFIA) & mtH;
 
         // directory entry + memory (ref :222,234 :304,517 :346,456 :561 :615)
-        const bool to_req = (RR & dsU) | WRQ | UPG;
-        uint32_t nbv = (RR & dsS) ? (bv | sbit) : bv;
-        nbv = to_req ? sbit : nbv;
-        nbv = homeH ? ((FIA ? 0u : bv) | (1u << msr)) : nbv;
-        nbv = esH ? es_bv : nbv;
-        nbv = EMOD ? 0u : nbv;
-        uint32_t nds = (to_req | (es_one)) ? (uint32_t)D_EM : ds;
-        nds = (FLUSH & tH) ? (uint32_t)D_S : nds;
-        nds = (EMOD | (esH & (es_pop == 0u))) ? (uint32_t)D_U : nds;
-        const uint32_t nmem = (homeH | EMOD) ? mval : mem;  // :307 :520 :602
+        const mask_t mToReq = (mRR & mU) | mWRQ | mUPG;
+        uint32_t nbv = B(mRR & mS) ? (bv | sbit) : bv;
+        nbv = B(mToReq) ? sbit : nbv;
+        nbv = B(mHomeH) ? ((B(mFIA) ? 0u : bv) | (1u << msr)) : nbv;
+        nbv = B(mEsH) ? es_bv : nbv;
+        nbv = B(mEMOD) ? 0u : nbv;
+        uint32_t nds = B(mToReq | mEsOne) ? (uint32_t)D_EM : ds;
+        nds = B(mFLUSH & mtH) ? (uint32_t)D_S : nds;
+        nds = B(mEMOD | (mEsH & M(es_pop == 0u))) ? (uint32_t)D_U : nds;
+        const uint32_t nmem = B(mHomeH | mEMOD) ? mval : mem;  // :307 :520 :602
 
-        // cache line
-        const bool fill = RRD | RWR | RID | ((FLUSH | FIA) & tSR) | own_hit;
-        const uint32_t fval = (RRD | FLUSH) ? mval : (iW ? ival : last_val);
-        const uint32_t fst = RRD ? (mds_s ? ST_S : ST_E) : (FLUSH ? ST_S : ST_M);
-        const bool own_home = es_own == H;
-        uint32_t nst = ((INV & same) | WBINV) ? ST_I : lst;               // :396-398 :501
-        nst = WBINT ? ST_S : nst;                                         // :284
-        nst = (ES & (!tH | (es_one & own_home))) ? ST_E : nst;            // :558 :586
-        nst = fill ? fst : nst;
+        // cache line: the new state by the value it takes (the type sets are disjoint)
+        const mask_t mFill = mRRD | mRWR | mRID | ((mFLUSH | mFIA) & mtSR) | mOwnHit;
+        const uint32_t fval = B(mRRD | mFLUSH) ? mval : (B(miW) ? ival : last_val);
+        const mask_t mDsS = M((m & (1u << 27)) != 0);     // REPLY_RD's dirState == S
+        const mask_t mOwnHome = M(es_own == H);
+        const mask_t mToI = (mINV & mSame) | mWBINV;                                   // :396-398 :501
+        const mask_t mToS = mWBINT | (mRRD & mDsS) | (mFLUSH & mtSR);                  // :284 :252 :319
+        const mask_t mToE = (mES & (~mtH | (mEsOne & mOwnHome))) | (mRRD & ~mDsS);     // :558 :586 :252
+        const mask_t mToM = mRWR | mRID | (mFIA & mtSR) | mOwnHit;                     // :470 :383 :531 :709
+        uint32_t nst = B(mToM) ? (uint32_t)ST_M : lst;
+        nst = B(mToE) ? (uint32_t)ST_E : nst;
+        nst = B(mToS) ? (uint32_t)ST_S : nst;
+        nst = B(mToI) ? (uint32_t)ST_I : nst;
         // handleCacheReplacement of the refilled line (:767-804); REPLY_WR unconditional (:467)
-        const bool ev = fill & !lI & (RWR | !same);
+        const mask_t mEv = mFill & ~mlI & (mRWR | ~mSame);
 
         // primary outgoing message: the handler's reply/forward, or else the eviction
         // notice -- no handler sends both (fills never reply), so one slot serves both
-        const bool vA = (req & !ctz0) | UPG | WBINV | WBINT | (es_one & !own_home) | (iR & !hit) | (iW & !own_hit);
-        uint32_t dA = (req | UPG) ? msender : H;
-        dA = em_req ? (uint32_t)__builtin_ctz(bv | 0x100u) : dA;
-        dA = esH ? es_own : dA;
-        // reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue: :666-734)
-        uint32_t tA = iR ? (uint32_t)T_RR : (uint32_t)T_WRQ;
-        tA = (iW & hit) ? (uint32_t)T_UPG : tA;
-        tA = UPG ? (uint32_t)T_RID : tA;
-        tA = WBINV ? (uint32_t)T_FIA : tA;
-        tA = WBINT ? (uint32_t)T_FLUSH : tA;
-        tA = ES ? (uint32_t)T_ES : tA;
-        tA = RR ? (dsEM ? (uint32_t)T_WBINT : (uint32_t)T_RRD) : tA;
-        tA = WRQ ? (dsEM ? (uint32_t)T_WBINV : (dsU ? (uint32_t)T_RWR : (uint32_t)T_RID)) : tA;
-        uint32_t valA = (WBINV | WBINT) ? lval : mem;
-        valA = do_issue ? ival : valA;
-        valA = (UPG | (WRQ & !dsEM)) ? es_bv : valA;
-        valA = (WRQ & dsEM) ? mval : valA;
-        const uint32_t srA = (WBINV | WBINT) ? msr : msender;
-        const uint32_t wA = mk(tA, t, addr, valA, srA, dsS ? 1u : 0u);
+        const mask_t mVA = (mReq & ~mCtz0) | mUPG | mWBINV | mWBINT | (mEsOne & ~mOwnHome) | (miR & ~mHit) |
+                           (miW & ~mOwnHit);
+        uint32_t dA = B(mReq | mUPG) ? msender : H;
+        dA = B(mEmReq) ? (uint32_t)__builtin_ctz(bv | 0x100u) : dA;
+        dA = B(mEsH) ? es_own : dA;
+        // reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue: :666-734);
+        // REPLY_RD carries dirState == S in bit 27 (the other receivers ignore it)
+        uint32_t tA = B(miR) ? (uint32_t)T_RR : (uint32_t)T_WRQ;
+        tA = B(miW & mHit) ? (uint32_t)T_UPG : tA;
+        tA = B(mUPG | (mWRQ & mS)) ? (uint32_t)T_RID : tA;
+        tA = B(mWBINV) ? (uint32_t)T_FIA : tA;
+        tA = B(mWBINT) ? (uint32_t)T_FLUSH : tA;
+        tA = B(mES) ? (uint32_t)T_ES : tA;
+        tA = B(mRR & mEM) ? (uint32_t)T_WBINT : tA;
+        tA = B(mRR & mS) ? (uint32_t)T_RRD | (1u << 27) : tA;
+        tA = B(mRR & mU) ? (uint32_t)T_RRD : tA;
+        tA = B(mWRQ & mEM) ? (uint32_t)T_WBINV : tA;
+        tA = B(mWRQ & mU) ? (uint32_t)T_RWR : tA;
+        uint32_t valA = B(mWBINV | mWBINT) ? lval : mem;
+        valA = B(mDo) ? ival : valA;
+        valA = B(mUPG | (mWRQ & ~mEM)) ? es_bv : valA;
+        valA = B(mWRQ & mEM) ? mval : valA;
+        const uint32_t srA = B(mWBINV | mWBINT) ? msr : msender;
+        const uint32_t wA = tA | (t << 4) | (mw & 0x7F00u) | (valA << 16) | (srA << 24);
         const uint32_t dE = laddr >> 4;
-        const bool inN = laddr < N * 16u;  // home node of the evicted line exists
-        const bool vE = ev & inN;
-        const uint32_t wE = (lst == ST_M ? wEM : wES) | (c16 << 8);
-        const bool vP = vA | vE;
-        const uint32_t dP = (vA ? dA : dE) & 7u;
-        const uint32_t wP = vA ? wA : wE;
+        const mask_t mInN = M(laddr < N * 16u);  // home node of the evicted line exists
+        const uint32_t wE = (B(mlM) ? wEM : wES) | (c16 << 8);
+        const mask_t mVP = mVA | (mEv & mInN);
+        const uint32_t dP = B(mVA) ? dA : dE;
+        const uint32_t wP = B(mVA) ? wA : wE;
         // second copy of a flush: WRITEBACK_INV always (:498), WRITEBACK_INT if sr != home (:281)
-        const bool vB = WBINV | (WBINT & (H != msr));
+        const mask_t mVB = mWBINV | (mWBINT & M(H != msr));
 
-        wmask = vote((iR & !hit) | (iW & !own_hit)) | (wmask & ~vote(RRD | RWR | RID | FLUSH | FIA));
-        last_val = do_issue ? ival : last_val;
-        const bool oob = ev & !inN;  // ref UB: messageBuffers[15] -> drop + flag
-        if (oob | ctz0) {  // rare: keep the counting off the common path
+        wmask = (miR & ~mHit) | (miW & ~mOwnHit) | (wmask & ~(mRRD | mRWR | mRID | mFLUSH | mFIA));
+        last_val = B(mDo) ? ival : last_val;
+        const mask_t mOob = mEv & ~mInN;  // ref UB: messageBuffers[15] -> drop + flag
+        if ((mOob | mCtz0) != 0) {        // rare: one wave-uniform test keeps it off the common path
             COLD();
-            err |= (oob ? DASH_ERR_OOB_D : 0u) | (ctz0 ? DASH_ERR_CTZ0_D : 0u);
-            drops += (oob ? 1u : 0u) + (ctz0 ? 1u : 0u);
+            err |= (B(mOob) ? DASH_ERR_OOB_D : 0u) | (B(mCtz0) ? DASH_ERR_CTZ0_D : 0u);
+            drops += (B(mOob) ? 1u : 0u) + (B(mCtz0) ? 1u : 0u);
         }
 
         *ent = (uint16_t)(nmem | (nbv << 8));
-        *cac = (uint16_t)(fill ? (addr | (fval << 8)) : c16);
+        *cac = (uint16_t)(B(mFill) ? (addr | (fval << 8)) : c16);
         dsv = (dsv & ~(3u << (2 * b))) | (nds << (2 * b));
         cst = (cst & ~(3u << (2 * idx))) | (nst << (2 * idx));
 
@@ -437,17 +454,20 @@ void sim_kernel(const SimArgs a) {
         // compares the receiver's count plus that rank with the ring depth.
         lds[L::MQ + 2 * lane + 1] = tq | (cq << 8);  // tail (with ring column) | count << 16
         const uint32_t bitP = bitI << 1, bitB = bitI << 2;
-        if (vP)
+        if (B(mVP))
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (vB)
+        if (B(mVB))
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (RID) {  // REPLY_ID's INV fan-out (ref :364-373): ascending receivers
+        // REPLY_ID's INV fan-out (ref :364-373), ascending receivers: one wave-uniform test
+        // guards both of its loops (arrival bits here, ring stores after the other sends)
+        const bool anyRID = mRID != 0;
+        if (anyRID && B(mRID)) {
             COLD();
             for (uint32_t im = mval & rcv_mask; im != 0; im &= im - 1u)
                 __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + (uint32_t)__builtin_ctz(im))], bitI,
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        auto place = [&](bool v, uint32_t d, uint32_t bit, uint32_t w) {
+        auto place = [&](mask_t v, uint32_t d, uint32_t bit, uint32_t w) {
             const uint2 q = *reinterpret_cast<const uint2*>(&lds[L::MQ + 2 * (seg + d)]);
             const uint32_t rank = (uint32_t)__builtin_popcount(q.x & (bit - 1u));
             // slot byte offset = receiver tail + rank slots, in the receiver's ring
@@ -455,32 +475,24 @@ void sim_kernel(const SimArgs a) {
             // fall off the mask
             const uint32_t off = (q.y + (rank << 8)) & RMASK;
             if constexpr (FINAL) {
-                const bool ok = v & ((q.y >> 16) + rank < RING);
-#if DASH_MASKED_STORE
-                if (ok) *reinterpret_cast<uint32_t*>(ldsb + L::RNG * 4 + off) = w;
-#else
-                *reinterpret_cast<uint32_t*>(ldsb + (ok ? L::RNG * 4 + off : L::DUM * 4 + lane * 4)) = w;
-#endif
-                if (vote(v & !ok) != 0) {
+                const mask_t ok = v & M((q.y >> 16) + rank < RING);
+                if (B(ok)) *reinterpret_cast<uint32_t*>(ldsb + L::RNG * 4 + off) = w;
+                if ((v & ~ok) != 0) {
                     COLD();
-                    err |= (v & !ok) ? DASH_ERR_OVERFLOW_D : 0u;
-                    drops += (v & !ok) ? 1u : 0u;
+                    err |= B(v & ~ok) ? DASH_ERR_OVERFLOW_D : 0u;
+                    drops += B(v & ~ok) ? 1u : 0u;
                 }
             } else {
-#if DASH_MASKED_STORE
-                if (v) *reinterpret_cast<uint32_t*>(ldsb + L::RNG * 4 + off) = w;
-#else
-                *reinterpret_cast<uint32_t*>(ldsb + (v ? L::RNG * 4 + off : L::DUM * 4 + lane * 4)) = w;
-#endif
+                if (B(v)) *reinterpret_cast<uint32_t*>(ldsb + L::RNG * 4 + off) = w;
             }
         };
-        place(vP, dP, bitP, wP);
-        place(vB, msr, bitB, wA);
-        if (RID) {
+        place(mVP, dP, bitP, wP);
+        place(mVB, msr, bitB, wA);
+        if (anyRID && B(mRID)) {
             COLD();
             const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
             for (uint32_t im = mval & rcv_mask; im != 0; im &= im - 1u)
-                place(true, (uint32_t)__builtin_ctz(im), bitI, winv);
+                place(M(true), (uint32_t)__builtin_ctz(im), bitI, winv);
         }
         const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQ + 2 * lane], 0u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -650,7 +662,7 @@ static uint32_t lds_pad() {
 
 template <int P, int CS, uint32_t RING>
 static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t s) {
-    if (a.arb_seed)
+    if (a.arb_seed || a.events)
         hipLaunchKernelGGL((sim_kernel<P, CS, RING, true>), dim3((uint32_t)groups), dim3(64), lds_pad(), s, a);
     else
         hipLaunchKernelGGL((sim_kernel<P, CS, RING, false>), dim3((uint32_t)groups), dim3(64), lds_pad(), s, a);
@@ -682,6 +694,9 @@ static hipError_t launch_sim_p(const SimArgs& a, uint32_t cs, uint32_t ring, uin
 hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring, uint64_t groups,
                       hipStream_t s) {
     if (groups == 0) return hipSuccess;
+#ifdef DASH_HEADLINE_ONLY  // quick experiment builds (tools/): the headline kernels only
+    return seg == 8 && cs == 4 ? launch_sim_pc<8, 4>(a, ring, groups, s) : hipErrorInvalidValue;
+#else
     switch (seg) {
     case 1: return launch_sim_p<1>(a, cs, ring, groups, s);
     case 2: return launch_sim_p<2>(a, cs, ring, groups, s);
@@ -689,6 +704,7 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring
     case 8: return launch_sim_p<8>(a, cs, ring, groups, s);
     default: return hipErrorInvalidValue;
     }
+#endif
 }
 
 __global__ __launch_bounds__(256) void clear_rd_kernel(uint2* trace, uint64_t words) {

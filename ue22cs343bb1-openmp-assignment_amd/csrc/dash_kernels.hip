@@ -203,91 +203,42 @@ void sim_kernel(const SimArgs a) {
     uint32_t err = 0, maxd = 0, drops = 0;  // maxd in ring-slot bytes until the end
     uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
     uint32_t nev = 0;         // events logged (DEBUG_MSG / DEBUG_INSTR emission, off unless a.events)
-    const uint32_t cap = a.max_rounds;
+    // loop-invariant uniform values a round needs, kept in VGPRs: the round's lane masks
+    // need the SGPRs (spilling them costs VALU)
+    uint32_t cap = a.max_rounds, nlim = N * 16u, rcv_all = rcv_mask;
+    asm volatile("" : "+v"(cap), "+v"(nlim), "+v"(rcv_all));
 
     const uint32_t wES = T_ES | (t << 4), wEM = T_EMOD | (t << 4);  // eviction notice, sender part
 
-    uint32_t r = 0;
+    // round counter: rv (a VGPR copy, so the lane masks keep the SGPRs) is the round of
+    // the trip's first step; the step at position k of the trip is round rv + k
+    uint32_t rv = 0;
+    asm volatile("" : "+v"(rv));
     const uint32_t sw2 = sw * 2u;  // byte offset of this lane's u16 in a 128-B row
-    // WCHUNK rounds per trip, unrolled: the housekeeping point (refill, quiescence vote,
-    // overflow stop) is the first round of every trip, a compile-time position
-    static_assert(DASH_QCHECK == WCHUNK, "one housekeeping point per WCHUNK rounds");
-    for (bool done = false; !done;)
-#pragma unroll
-    for (uint32_t k = 0; k < WCHUNK; ++k, ++r) {
-        // Every predicate below is a wave-wide lane mask (an SGPR pair): one compare makes
-        // it, the scalar unit combines them, v_cndmask consumes them. The kernel is bound by
-        // VALU issue, so no predicate is ever materialised in a VGPR.
-        // ---- quiescence / round cap, on start-of-round state ----
+
+    // Every predicate of a step is a wave-wide lane mask (an SGPR pair): one compare makes
+    // it, the scalar unit combines them, v_cndmask consumes them. The kernel is bound by
+    // VALU issue, so no predicate is ever materialised in a VGPR.
+    // Start-of-round state: a node can pop when its queue is non-empty -- at the final
+    // (reference-depth) tier a queue that reached MSG_BUFFER_SIZE has head == tail and the
+    // reference's drain loop (ref :167-170) never pops it again -- and can issue when it is
+    // not waitingForReply (ref :624-629) and has instructions left.
+    auto can_pop = [&]() -> mask_t { return FINAL ? M(cq != 0) & M(cq != RING * SLOT) : M(cq != 0); };
+    auto can_issue = [&]() -> mask_t { return M(pc < lenx) & ~wmask; };
+
+    // one lockstep round (WCHUNK of them per trip, unrolled)
+    auto step = [&](const uint32_t k, const mask_t mMsg, const mask_t mIss) __attribute__((always_inline)) {
         // A system is active while any of its nodes has a message or can issue;
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
-        mask_t mIss = M(pc < lenx) & ~wmask;  // not waitingForReply (ref :624-629), instructions left
-        // the final (reference-depth) tier: a queue that reached MSG_BUFFER_SIZE has
-        // head == tail, so the reference's drain loop (ref :167-170) never pops it again
-        mask_t mMsg = FINAL ? M(cq != 0) & M(cq != RING * SLOT) : M(cq != 0);
-        mask_t mAct = mMsg | mIss;
-        // the round cap is a multiple of WCHUNK (dash_create rounds it up), so it can only
-        // fall on a trip's first round
-        if (k == 0 && r == cap) {  // wave-uniform: every system still active has run `cap` rounds
+        if (B(mMsg | mIss)) {
             COLD();
-            const bool kill = ((uint32_t)(mAct >> seg) & SEGMASK) != 0;
-            const mask_t mKill = M(kill);
-            wmask &= ~mKill;
-            mMsg &= ~mKill;
-            mIss &= ~mKill;
-            mAct &= ~mKill;
-            if (kill) {
-                err |= DASH_ERR_ROUNDCAP_D;
-                cq = 0;
-                lenx = pc;
-            }
+            last_act = rv + k;
         }
-        if (B(mAct)) {
-            COLD();
-            last_act = r;
-        }
-
-        // ---- wave-uniform housekeeping: trace window refill ----
-        // Invariant at a refill point: pend_idx >= pc/WCHUNK + 1 and the window holds
-        // chunks pend_idx-2 and pend_idx-1. pc advances <= WCHUNK per WCHUNK rounds, so
-        // the chunks read until the next refill point (pc/WCHUNK, pc/WCHUNK + 1) are
-        // always resident; the pending chunk's load has WCHUNK rounds to land.
-        if (k == 0) {
-            // quiescence is absorbing, so testing it once per trip only adds idle
-            // rounds (no state changes, not counted in `rounds`)
-            if (mAct == 0) {
-                done = true;
-                break;
-            }
-            // a non-final tier stops a system soon after its first overflow: it will be
-            // re-simulated from scratch at the next depth, its results here are void
-            if (!FINAL) {
-                const mask_t ovf = M(maxd > RING * SLOT);
-                if (ovf != 0) {
-                    COLD();
-                    const bool stop = ((uint32_t)(ovf >> seg) & SEGMASK) != 0;
-                    const mask_t mStop = M(stop);
-                    wmask &= ~mStop;
-                    mMsg &= ~mStop;
-                    mIss &= ~mStop;
-                    if (stop) {
-                        cq = 0;
-                        lenx = pc;
-                    }
-                }
-            }
-            if (pend_idx < nch && pend_idx < pc / (WCHUNK * PCU) + WIN) {
-                put_chunk(pend_idx, pend);
-                ++pend_idx;
-                if (pend_idx < nch) pend = tr[pend_idx];
-            }
-        }
-
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
         mask_t mStall = 0;
         uint32_t bitI = 1u << (4 * t);
         if (SLOW && a.arb_seed) {  // round keys are wave-uniform: computed on the scalar unit
-            const uint64_t rk = a.arb_seed ^ ((uint64_t)r * 0x9E3779B97F4A7C15ull);
+            const uint64_t rk = a.arb_seed ^ ((uint64_t)__builtin_amdgcn_readfirstlane(rv + k) * 0x9E3779B97F4A7C15ull);
             const uint64_t key = fmix64(rk), skey = fmix64(rk ^ 0xD1B54A32D192ED03ull);
             mStall = M(((skey >> (8 * t)) & 3u) == 0);
             const uint32_t A = ((uint32_t)key & (P - 1)) | 1u, Bc = (uint32_t)(key >> 8) & (P - 1);
@@ -323,7 +274,7 @@ void sim_kernel(const SimArgs a) {
             if (B(mHas | mDo)) {
                 if (nev < a.event_cap) {
                     uint32_t* e = a.events + ((sys * N + t) * a.event_cap + nev) * 2;
-                    e[0] = r;
+                    e[0] = rv + k;
                     e[1] = B(mHas) ? m : (ins | 0x80000000u);
                 }
                 ++nev;
@@ -421,7 +372,7 @@ void sim_kernel(const SimArgs a) {
         const uint32_t srA = B(mWBINV | mWBINT) ? msr : msender;
         const uint32_t wA = tA | (t << 4) | (mw & 0x7F00u) | (valA << 16) | (srA << 24);
         const uint32_t dE = laddr >> 4;
-        const mask_t mInN = M(laddr < N * 16u);  // home node of the evicted line exists
+        const mask_t mInN = M(laddr < nlim);  // home node of the evicted line exists
         const uint32_t wE = (B(mlM) ? wEM : wES) | (c16 << 8);
         const mask_t mVP = mVA | (mEv & mInN);
         const uint32_t dP = B(mVA) ? dA : dE;
@@ -463,7 +414,7 @@ void sim_kernel(const SimArgs a) {
         const bool anyRID = mRID != 0;
         if (anyRID && B(mRID)) {
             COLD();
-            for (uint32_t im = mval & rcv_mask; im != 0; im &= im - 1u)
+            for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
                 __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + (uint32_t)__builtin_ctz(im))], bitI,
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -491,7 +442,7 @@ void sim_kernel(const SimArgs a) {
         if (anyRID && B(mRID)) {
             COLD();
             const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
-            for (uint32_t im = mval & rcv_mask; im != 0; im &= im - 1u)
+            for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
                 place(M(true), (uint32_t)__builtin_ctz(im), bitI, winv);
         }
         const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQ + 2 * lane], 0u, __ATOMIC_RELAXED,
@@ -507,6 +458,60 @@ void sim_kernel(const SimArgs a) {
             }
         }
         maxd = max(maxd, cq);
+    };
+
+    // WCHUNK rounds per trip, unrolled; the trip's start is the housekeeping point
+    // (quiescence vote, round cap, overflow stop, trace window refill)
+    static_assert(DASH_QCHECK == WCHUNK, "one housekeeping point per WCHUNK rounds");
+    for (;; rv += WCHUNK) {
+        mask_t mMsg = can_pop(), mIss = can_issue();
+        // quiescence is absorbing, so testing it once per trip only adds idle rounds (no
+        // state changes, not counted in `rounds`)
+        if ((mMsg | mIss) == 0) break;
+        // the round cap is a multiple of WCHUNK (dash_create rounds it up), so it can only
+        // fall on a trip's first round
+        if (M(rv == cap) != 0) {  // wave-uniform: every system still active has run `cap` rounds
+            COLD();
+            const bool kill = ((uint32_t)((mMsg | mIss) >> seg) & SEGMASK) != 0;
+            const mask_t mKill = M(kill);
+            wmask &= ~mKill;
+            mMsg &= ~mKill;
+            mIss &= ~mKill;
+            if (kill) {
+                err |= DASH_ERR_ROUNDCAP_D;
+                cq = 0;
+                lenx = pc;
+            }
+        }
+        // a non-final tier stops a system soon after its first overflow: it will be
+        // re-simulated from scratch at the next depth, its results here are void
+        if (!FINAL) {
+            const mask_t ovf = M(maxd > RING * SLOT);
+            if (ovf != 0) {
+                COLD();
+                const bool stop = ((uint32_t)(ovf >> seg) & SEGMASK) != 0;
+                const mask_t mStop = M(stop);
+                wmask &= ~mStop;
+                mMsg &= ~mStop;
+                mIss &= ~mStop;
+                if (stop) {
+                    cq = 0;
+                    lenx = pc;
+                }
+            }
+        }
+        // trace window refill. Invariant here: pend_idx >= pc/WCHUNK + 1 and the window
+        // holds chunks pend_idx-2 and pend_idx-1. pc advances <= WCHUNK per WCHUNK rounds,
+        // so the chunks read until the next refill point (pc/WCHUNK, pc/WCHUNK + 1) are
+        // always resident; the pending chunk's load has WCHUNK rounds to land.
+        if (pend_idx < nch && pend_idx < pc / (WCHUNK * PCU) + WIN) {
+            put_chunk(pend_idx, pend);
+            ++pend_idx;
+            if (pend_idx < nch) pend = tr[pend_idx];
+        }
+        step(0, mMsg, mIss);
+#pragma unroll
+        for (uint32_t k = 1; k < WCHUNK; ++k) step(k, can_pop(), can_issue());
     }
 
     // ---- results ----
@@ -594,7 +599,7 @@ void sim_kernel(const SimArgs a) {
         if (ebits) atomicOr(&S[STAT_ERRBITS], (unsigned long long)ebits);
         if (s_drops) atomicAdd(&S[STAT_DROPS], (unsigned long long)s_drops);
         atomicMax(&S[STAT_MAXDEPTH], (unsigned long long)m_depth);
-        atomicAdd(&S[STAT_WAVE_ROUNDS], (unsigned long long)r);
+        atomicAdd(&S[STAT_WAVE_ROUNDS], (unsigned long long)__builtin_amdgcn_readfirstlane(rv));
     }
 }
 

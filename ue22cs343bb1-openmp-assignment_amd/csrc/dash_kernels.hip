@@ -209,6 +209,24 @@ void sim_kernel(const SimArgs a) {
     asm volatile("" : "+v"(cap), "+v"(nlim), "+v"(rcv_all));
 
     const uint32_t wES = T_ES | (t << 4), wEM = T_EMOD | (t << 4);  // eviction notice, sender part
+    // reply-type table, one entry per lane, read with ds_bpermute: entry (step type s, dir
+    // state d) at lane 4s + d. Step types: the message types, 13 = no step, 14 / 15 = issue
+    // RD / WR. READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue: :666-734;
+    // REPLY_RD carries dirState == S in bit 27.
+    const uint32_t tatab = [&] {
+        const uint32_t st = lane >> 2, d = lane & 3;
+        switch (st) {
+        case T_RR: return d == D_EM ? (uint32_t)T_WBINT : (uint32_t)T_RRD | (d == D_S ? 1u << 27 : 0u);
+        case T_WRQ: return d == D_EM ? (uint32_t)T_WBINV : (d == D_S ? (uint32_t)T_RID : (uint32_t)T_RWR);
+        case T_UPG: return (uint32_t)T_RID;
+        case T_WBINV: return (uint32_t)T_FIA;
+        case T_WBINT: return (uint32_t)T_FLUSH;
+        case T_ES: return (uint32_t)T_ES;
+        case 14: return (uint32_t)T_RR;
+        case 15: return (uint32_t)T_WRQ;  // UPGRADE on a hit (patched per lane)
+        default: return 0u;
+        }
+    }();
 
     // round counter: rv (a VGPR copy, so the lane masks keep the SGPRs) is the round of
     // the trip's first step; the step at position k of the trip is round rv + k
@@ -230,10 +248,7 @@ void sim_kernel(const SimArgs a) {
     auto step = [&](const uint32_t k, const mask_t mMsg, const mask_t mIss) __attribute__((always_inline)) {
         // A system is active while any of its nodes has a message or can issue;
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
-        if (B(mMsg | mIss)) {
-            COLD();
-            last_act = rv + k;
-        }
+        last_act = B(mMsg | mIss) ? rv + k : last_act;
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
         mask_t mStall = 0;
         uint32_t bitI = 1u << (4 * t);
@@ -269,6 +284,9 @@ void sim_kernel(const SimArgs a) {
         const uint32_t e16 = *ent;
         const uint32_t c16 = *cac;
         const uint32_t mty = m & 15u;
+        // the popped message's type, or 13 (no transactionType) for a lane that does not pop:
+        // the type masks below then need no AND with mHas
+        const uint32_t pty = B(mHas) ? mty : 13u;
         if (SLOW && a.events) {  // wave-uniform: the batch-of-1 trace (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652)
             COLD();
             if (B(mHas | mDo)) {
@@ -285,15 +303,15 @@ void sim_kernel(const SimArgs a) {
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
 
         // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
-        const mask_t mRR = mHas & M(mty == T_RR), mWRQ = mHas & M(mty == T_WRQ);
-        const mask_t mRRD = mHas & M(mty == T_RRD), mRWR = mHas & M(mty == T_RWR);
-        const mask_t mRID = mHas & M(mty == T_RID), mINV = mHas & M(mty == T_INV);
-        const mask_t mUPG = mHas & M(mty == T_UPG), mWBINV = mHas & M(mty == T_WBINV);
-        const mask_t mWBINT = mHas & M(mty == T_WBINT), mFLUSH = mHas & M(mty == T_FLUSH);
-        const mask_t mFIA = mHas & M(mty == T_FIA), mES = mHas & M(mty == T_ES);
-        const mask_t mEMOD = mHas & M(mty == T_EMOD);
-        const mask_t mIsW = M(ins >= 0x8000u);
-        const mask_t miR = mDo & ~mIsW, miW = mDo & mIsW;
+        const mask_t mRR = M(pty == T_RR), mWRQ = M(pty == T_WRQ);
+        const mask_t mRRD = M(pty == T_RRD), mRWR = M(pty == T_RWR);
+        const mask_t mRID = M(pty == T_RID), mINV = M(pty == T_INV);
+        const mask_t mUPG = M(pty == T_UPG), mWBINV = M(pty == T_WBINV);
+        const mask_t mWBINT = M(pty == T_WBINT), mFLUSH = M(pty == T_FLUSH);
+        const mask_t mFIA = M(pty == T_FIA), mES = M(pty == T_ES);
+        const mask_t mEMOD = M(pty == T_EMOD);
+        const uint32_t sty = B(mDo) ? (ins >> 15) | 14u : pty;  // step type: 14 / 15 = issue RD / WR
+        const mask_t miR = M(sty == 14u), miW = M(sty == 15u);
 
         const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
         const uint32_t laddr = c16 & 0xFFu, lval = c16 >> 8, lst = (cst >> (2 * idx)) & 3u;
@@ -331,7 +349,10 @@ void sim_kernel(const SimArgs a) {
 
         // cache line: the new state by the value it takes (the type sets are disjoint)
         const mask_t mFill = mRRD | mRWR | mRID | ((mFLUSH | mFIA) & mtSR) | mOwnHit;
-        const uint32_t fval = B(mRRD | mFLUSH) ? mval : (B(miW) ? ival : last_val);
+        // REPLY_WR / REPLY_ID / FLUSH_INVACK fill with the last issued value (:470,383,531),
+        // a WR hit with its own (= the new last value)
+        last_val = B(mDo) ? ival : last_val;
+        const uint32_t fval = B(mRRD | mFLUSH) ? mval : last_val;
         const mask_t mDsS = M((m & (1u << 27)) != 0);     // REPLY_RD's dirState == S
         const mask_t mOwnHome = M(es_own == H);
         const mask_t mToI = (mINV & mSame) | mWBINV;                                   // :396-398 :501
@@ -354,17 +375,8 @@ void sim_kernel(const SimArgs a) {
         dA = B(mEsH) ? es_own : dA;
         // reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue: :666-734);
         // REPLY_RD carries dirState == S in bit 27 (the other receivers ignore it)
-        uint32_t tA = B(miR) ? (uint32_t)T_RR : (uint32_t)T_WRQ;
+        uint32_t tA = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sty << 4) | (ds << 2)), (int)tatab);
         tA = B(miW & mHit) ? (uint32_t)T_UPG : tA;
-        tA = B(mUPG | (mWRQ & mS)) ? (uint32_t)T_RID : tA;
-        tA = B(mWBINV) ? (uint32_t)T_FIA : tA;
-        tA = B(mWBINT) ? (uint32_t)T_FLUSH : tA;
-        tA = B(mES) ? (uint32_t)T_ES : tA;
-        tA = B(mRR & mEM) ? (uint32_t)T_WBINT : tA;
-        tA = B(mRR & mS) ? (uint32_t)T_RRD | (1u << 27) : tA;
-        tA = B(mRR & mU) ? (uint32_t)T_RRD : tA;
-        tA = B(mWRQ & mEM) ? (uint32_t)T_WBINV : tA;
-        tA = B(mWRQ & mU) ? (uint32_t)T_RWR : tA;
         uint32_t valA = B(mWBINV | mWBINT) ? lval : mem;
         valA = B(mDo) ? ival : valA;
         valA = B(mUPG | (mWRQ & ~mEM)) ? es_bv : valA;
@@ -381,7 +393,6 @@ void sim_kernel(const SimArgs a) {
         const mask_t mVB = mWBINV | (mWBINT & M(H != msr));
 
         wmask = (miR & ~mHit) | (miW & ~mOwnHit) | (wmask & ~(mRRD | mRWR | mRID | mFLUSH | mFIA));
-        last_val = B(mDo) ? ival : last_val;
         const mask_t mOob = mEv & ~mInN;  // ref UB: messageBuffers[15] -> drop + flag
         if ((mOob | mCtz0) != 0) {        // rare: one wave-uniform test keeps it off the common path
             COLD();
@@ -403,7 +414,8 @@ void sim_kernel(const SimArgs a) {
         // ref :364-379): a sender's slot is the receiver's tail plus the number of
         // bits below its own, and the receiver's capacity check (ref :754-761)
         // compares the receiver's count plus that rank with the ring depth.
-        lds[L::MQ + 2 * lane + 1] = tq | (cq << 8);  // tail (with ring column) | count << 16
+        // tail (with ring column); the final tier adds count << 16 for the capacity check
+        lds[L::MQ + 2 * lane + 1] = FINAL ? tq | (cq << 8) : tq;
         const uint32_t bitP = bitI << 1, bitB = bitI << 2;
         if (B(mVP))
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -449,7 +461,8 @@ void sim_kernel(const SimArgs a) {
                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         uint32_t n = (uint32_t)__builtin_popcount(arrived) << 8;
         if constexpr (FINAL) n = min(n, RING * SLOT - cq);  // sendMessage's drop (ref :754-761)
-        tq = (tq + n) & RMASK;
+        // below the final tier tq is not wrapped here: every reader masks it with RMASK
+        tq = FINAL ? (tq + n) & RMASK : tq + n;
         cq += n;
         if constexpr (FINAL) {
             if (cq == RING * SLOT) {  // full: stuck for good (DASH_ERR_STUCK)

@@ -10,18 +10,16 @@ step tests
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1 \
   || { tail -20 "$OUT/tests.log"; exit 1; }
 tail -1 "$OUT/tests.log"
-step bench uniform
-timeout -k 10 400 python3 bench.py > "$OUT/bench_uniform.json" 2> "$OUT/bench_uniform.err" || exit 1
-step bench contention
-timeout -k 10 300 python3 bench.py --kind contention --no-cpu-baseline > "$OUT/bench_contention.json" 2> "$OUT/bench_contention.err" || exit 1
+step bench "(headline line: uniform + contention + CPU baselines)"
+timeout -k 10 400 python3 bench.py --steps 10 --warmup 2 > "$OUT/bench_uniform.json" 2> "$OUT/bench_uniform.err" || exit 1
 step kernel trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/trace.log" 2>&1 || exit 1
+    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --contention-steps 2 > "$OUT/trace.log" 2>&1 || exit 1
 pmc() {  # kind name counters...
   local kind=$1 name=$2; shift 2
   step pmc "$kind" "$name"
   timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/pmc_$kind/$name" -o run -- \
-      python3 bench.py --kind "$kind" --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc_$kind/$name.log" 2>&1 \
+      python3 bench.py --kind "$kind" --steps 1 --warmup 0 --no-cpu-baseline --contention-steps 0 > "$OUT/pmc_$kind/$name.log" 2>&1 \
       || { echo "pmc $name failed"; exit 1; }
 }
 for kind in uniform contention; do

@@ -91,8 +91,9 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
     static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
-    static constexpr uint32_t HST = WND + WIN * WCHUNK * 64 / 2;  // u32 [13][64/P+1] per-system counters
-    static constexpr uint32_t MQ = (HST + 13 * HSTRIDE + 1) & ~1u;  // u32 [64][2] arrivals mask, tail|count<<16
+    static constexpr uint32_t HST = WND + WIN * WCHUNK * 64 / 2;  // u32 [14][64/P+1] per-system counters (row 13: lanes without a message)
+    static constexpr uint32_t HROWS = 14;                   // 13 types + a row for lanes without a message
+    static constexpr uint32_t MQ = (HST + HROWS * HSTRIDE + 1) & ~1u;  // u32 [64][2] arrivals mask, tail|count<<16
     static constexpr uint32_t DUM = MQ + 2 * 64;            // u32 [64]      target of a suppressed store
     static constexpr uint32_t WORDS = DUM + (DASH_MASKED_STORE ? 0 : 64);
 };
@@ -155,7 +156,7 @@ void sim_kernel(const SimArgs a) {
     for (uint32_t b = 0; b < 16; ++b) lds16[L::ENT * 2 + b * 64 + sw] = (uint16_t)((20u * t + b) & 0xFFu);
 #pragma unroll
     for (uint32_t i = 0; i < ncs; ++i) lds16[L::CAC * 2 + i * 64 + sw] = 0xFFu;
-    for (uint32_t w = lane; w < 13 * L::HSTRIDE; w += 64) lds[L::HST + w] = 0u;
+    for (uint32_t w = lane; w < L::HROWS * L::HSTRIDE; w += 64) lds[L::HST + w] = 0u;
     lds[L::MQ + 2 * lane] = 0u;
     char* const ldsb = reinterpret_cast<char*>(lds);
     constexpr uint32_t SLOT = 64 * 4;                 // bytes per ring slot (one word per lane)
@@ -298,9 +299,10 @@ void sim_kernel(const SimArgs a) {
                 ++nev;
             }
         }
-        if (B(mHas))  // messages handled per transactionType, per system
-            __hip_atomic_fetch_add(&lds[L::HST + mty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        // messages handled per transactionType, per system; a lane without a message counts
+        // into the unused row 13, so no exec mask is needed
+        __hip_atomic_fetch_add(&lds[L::HST + pty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
 
         // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
         const mask_t mRR = M(pty == T_RR), mWRQ = M(pty == T_WRQ);

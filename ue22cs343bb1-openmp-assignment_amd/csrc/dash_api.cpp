@@ -501,14 +501,16 @@ int dash_read_events(dash_t* h, uint64_t sys, dash_event* out, uint32_t cap, uin
         int best = -1;
         for (uint32_t t = 0; t < N; t++) {
             if (pos[t] >= std::min(cnt[t], E)) continue;
-            if (best < 0 || ev[((size_t)t * E + pos[t]) * 2] < ev[((size_t)best * E + pos[best]) * 2]) best = (int)t;
+            if (best < 0 || (ev[((size_t)t * E + pos[t]) * 2] & 0x7FFFFFFFu) <
+                                (ev[((size_t)best * E + pos[best]) * 2] & 0x7FFFFFFFu))
+                best = (int)t;
         }
         if (best < 0) break;
         const uint32_t* e = &ev[((size_t)best * E + pos[best]) * 2];
         if (k < cap) {
-            out[k].round = e[0];
+            out[k].round = e[0] & 0x7FFFFFFFu;  // bit 31: an issued instruction
             out[k].node = (uint32_t)best;
-            out[k].kind = (e[1] & 0x80000000u) ? DASH_EV_INSTR : DASH_EV_MSG;
+            out[k].kind = (e[0] & 0x80000000u) ? DASH_EV_INSTR : DASH_EV_MSG;
             out[k].word = e[1] & 0x7FFFFFFFu;
         }
         ++k;

@@ -210,21 +210,24 @@ void sim_kernel(const SimArgs a) {
     asm volatile("" : "+v"(cap), "+v"(nlim), "+v"(rcv_all));
 
     const uint32_t wES = T_ES | (t << 4), wEM = T_EMOD | (t << 4);  // eviction notice, sender part
-    // reply-type table, one entry per lane, read with ds_bpermute: entry (step type s, dir
-    // state d) at lane 4s + d. Step types: the message types, 13 = no step, 14 / 15 = issue
-    // RD / WR. READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue: :666-734;
-    // REPLY_RD carries dirState == S in bit 27.
+    // reply table, one entry per lane, read with ds_bpermute: entry (step type s, dir state
+    // d) at lane 4s + d. Step types: the message types, 13 = no step, 14 / 15 = issue RD / WR.
+    // Bits 3..0: the reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue:
+    // :666-734); bit 27: REPLY_RD's dirState == S; bit 31 (SENDS): the step sends that reply,
+    // subject to the per-lane conditions applied after the lookup (ctz(0), hits). Receivers
+    // ignore bits 28..31 of a message word.
+    constexpr uint32_t SENDS = 1u << 31;
     const uint32_t tatab = [&] {
         const uint32_t st = lane >> 2, d = lane & 3;
         switch (st) {
-        case T_RR: return d == D_EM ? (uint32_t)T_WBINT : (uint32_t)T_RRD | (d == D_S ? 1u << 27 : 0u);
-        case T_WRQ: return d == D_EM ? (uint32_t)T_WBINV : (d == D_S ? (uint32_t)T_RID : (uint32_t)T_RWR);
-        case T_UPG: return (uint32_t)T_RID;
-        case T_WBINV: return (uint32_t)T_FIA;
-        case T_WBINT: return (uint32_t)T_FLUSH;
-        case T_ES: return (uint32_t)T_ES;
-        case 14: return (uint32_t)T_RR;
-        case 15: return (uint32_t)T_WRQ;  // UPGRADE on a hit (patched per lane)
+        case T_RR: return SENDS | (d == D_EM ? (uint32_t)T_WBINT : (uint32_t)T_RRD | (d == D_S ? 1u << 27 : 0u));
+        case T_WRQ: return SENDS | (d == D_EM ? (uint32_t)T_WBINV : (d == D_S ? (uint32_t)T_RID : (uint32_t)T_RWR));
+        case T_UPG: return SENDS | (uint32_t)T_RID;
+        case T_WBINV: return SENDS | (uint32_t)T_FIA;
+        case T_WBINT: return SENDS | (uint32_t)T_FLUSH;
+        case T_ES: return (uint32_t)T_ES;  // sent only when the entry drops to one sharer elsewhere
+        case 14: return SENDS | (uint32_t)T_RR;
+        case 15: return SENDS | (uint32_t)T_WRQ;  // UPGRADE on a hit (patched per lane)
         default: return 0u;
         }
     }();
@@ -234,6 +237,9 @@ void sim_kernel(const SimArgs a) {
     uint32_t rv = 0;
     asm volatile("" : "+v"(rv));
     const uint32_t sw2 = sw * 2u;  // byte offset of this lane's u16 in a 128-B row
+#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU)
+    uint32_t padv[4] = {lane, lane + 1, lane + 2, lane + 3}, pads[4] = {0, 1, 2, 3};
+#endif
 
     // Every predicate of a step is a wave-wide lane mask (an SGPR pair): one compare makes
     // it, the scalar unit combines them, v_cndmask consumes them. The kernel is bound by
@@ -293,8 +299,8 @@ void sim_kernel(const SimArgs a) {
             if (B(mHas | mDo)) {
                 if (nev < a.event_cap) {
                     uint32_t* e = a.events + ((sys * N + t) * a.event_cap + nev) * 2;
-                    e[0] = rv + k;
-                    e[1] = B(mHas) ? m : (ins | 0x80000000u);
+                    e[0] = (rv + k) | (B(mHas) ? 0u : 0x80000000u);  // bit 31: an issued instruction
+                    e[1] = B(mHas) ? m : ins;
                 }
                 ++nev;
             }
@@ -304,6 +310,18 @@ void sim_kernel(const SimArgs a) {
         __hip_atomic_fetch_add(&lds[L::HST + pty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
 
+#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU)  // issue-cost probes (tools/ only)
+        {
+#ifdef DASH_PAD_VALU
+            asm volatile(".rept %4\n v_add_u32 %0, 1, %0\n v_add_u32 %1, 1, %1\n v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n .endr"
+                         : "+v"(padv[0]), "+v"(padv[1]), "+v"(padv[2]), "+v"(padv[3]) : "i"(DASH_PAD_VALU / 4));
+#endif
+#ifdef DASH_PAD_SALU
+            asm volatile(".rept %4\n s_add_u32 %0, 1, %0\n s_add_u32 %1, 1, %1\n s_add_u32 %2, 1, %2\n s_add_u32 %3, 1, %3\n .endr"
+                         : "+s"(pads[0]), "+s"(pads[1]), "+s"(pads[2]), "+s"(pads[3]) : "i"(DASH_PAD_SALU / 4));
+#endif
+        }
+#endif
         // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
         const mask_t mRR = M(pty == T_RR), mWRQ = M(pty == T_WRQ);
         const mask_t mRRD = M(pty == T_RRD), mRWR = M(pty == T_RWR);
@@ -341,7 +359,10 @@ void sim_kernel(const SimArgs a) {
         const mask_t mToReq = (mRR & mU) | mWRQ | mUPG;
         uint32_t nbv = B(mRR & mS) ? (bv | sbit) : bv;
         nbv = B(mToReq) ? sbit : nbv;
-        nbv = B(mHomeH) ? ((B(mFIA) ? 0u : bv) | (1u << msr)) : nbv;
+        // computed unconditionally (kept out of a branch the compiler would otherwise form)
+        uint32_t hbv = (B(mFIA) ? 0u : bv) | (1u << msr);
+        asm volatile("" : "+v"(hbv));
+        nbv = B(mHomeH) ? hbv : nbv;
         nbv = B(mEsH) ? es_bv : nbv;
         nbv = B(mEMOD) ? 0u : nbv;
         uint32_t nds = B(mToReq | mEsOne) ? (uint32_t)D_EM : ds;
@@ -370,14 +391,14 @@ void sim_kernel(const SimArgs a) {
 
         // primary outgoing message: the handler's reply/forward, or else the eviction
         // notice -- no handler sends both (fills never reply), so one slot serves both
-        const mask_t mVA = (mReq & ~mCtz0) | mUPG | mWBINV | mWBINT | (mEsOne & ~mOwnHome) | (miR & ~mHit) |
-                           (miW & ~mOwnHit);
+        uint32_t tA = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sty << 4) | (ds << 2)), (int)tatab);
+        // a hit needs no request (:676-677, :706-710), except a WR hit on SHARED (UPGRADE)
+        const mask_t mVA = (M((int32_t)tA < 0) & ~mCtz0 & ~((miR & mHit) | mOwnHit)) | (mEsOne & ~mOwnHome);
         uint32_t dA = B(mReq | mUPG) ? msender : H;
         dA = B(mEmReq) ? (uint32_t)__builtin_ctz(bv | 0x100u) : dA;
         dA = B(mEsH) ? es_own : dA;
         // reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue: :666-734);
         // REPLY_RD carries dirState == S in bit 27 (the other receivers ignore it)
-        uint32_t tA = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sty << 4) | (ds << 2)), (int)tatab);
         tA = B(miW & mHit) ? (uint32_t)T_UPG : tA;
         uint32_t valA = B(mWBINV | mWBINT) ? lval : mem;
         valA = B(mDo) ? ival : valA;
@@ -394,7 +415,9 @@ void sim_kernel(const SimArgs a) {
         // second copy of a flush: WRITEBACK_INV always (:498), WRITEBACK_INT if sr != home (:281)
         const mask_t mVB = mWBINV | (mWBINT & M(H != msr));
 
-        wmask = (miR & ~mHit) | (miW & ~mOwnHit) | (wmask & ~(mRRD | mRWR | mRID | mFLUSH | mFIA));
+        // an issue that sends a request waits for its reply (:687, :723, :733); replies clear
+        // waitingForReply, and so do FLUSH and FLUSH_INVACK at any receiver (:254,473,386,322,535)
+        wmask = (mVA & mDo) | (wmask & ~(mRRD | mRWR | mRID | mFLUSH | mFIA));
         const mask_t mOob = mEv & ~mInN;  // ref UB: messageBuffers[15] -> drop + flag
         if ((mOob | mCtz0) != 0) {        // rare: one wave-uniform test keeps it off the common path
             COLD();
@@ -423,10 +446,9 @@ void sim_kernel(const SimArgs a) {
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (B(mVB))
             __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // REPLY_ID's INV fan-out (ref :364-373), ascending receivers: one wave-uniform test
-        // guards both of its loops (arrival bits here, ring stores after the other sends)
-        const bool anyRID = mRID != 0;
-        if (anyRID && B(mRID)) {
+        // REPLY_ID's INV fan-out (ref :364-373), ascending receivers: a wave-uniform test
+        // guards each of its loops (arrival bits here, ring stores after the other sends)
+        if (mRID != 0 && B(mRID)) {
             COLD();
             for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
                 __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + (uint32_t)__builtin_ctz(im))], bitI,
@@ -453,7 +475,7 @@ void sim_kernel(const SimArgs a) {
         };
         place(mVP, dP, bitP, wP);
         place(mVB, msr, bitB, wA);
-        if (anyRID && B(mRID)) {
+        if (mRID != 0 && B(mRID)) {
             COLD();
             const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
             for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
@@ -566,6 +588,9 @@ void sim_kernel(const SimArgs a) {
         a.errors[sys] = serr;
     }
     if (live && t == 0 && handoff) a.ovf_list[atomicAdd(a.ovf_count, 1u)] = (uint32_t)sys;
+#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU)
+    if (padv[0] + padv[1] + padv[2] + padv[3] + pads[0] + pads[1] + pads[2] + pads[3] == 0x7FFFFFFFu) a.stats[31] = 1;
+#endif
     if (a.events && report) a.event_count[sys * N + t] = nev;
     maxd >>= 8;  // ring-slot bytes -> messages
     if (a.state && report) {

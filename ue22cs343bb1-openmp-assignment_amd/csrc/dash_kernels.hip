@@ -91,10 +91,14 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
     static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
-    static constexpr uint32_t HST = WND + WIN * WCHUNK * 64 / 2;  // u32 [14][64/P+1] per-system counters (row 13: lanes without a message)
-    static constexpr uint32_t HROWS = 14;                   // 13 types + a row for lanes without a message
-    static constexpr uint32_t MQ = (HST + HROWS * HSTRIDE + 1) & ~1u;  // u32 [64][2] arrivals mask, tail|count<<16
-    static constexpr uint32_t DUM = MQ + 2 * 64;            // u32 [64]      target of a suppressed store
+    static constexpr uint32_t HST = WND + WIN * WCHUNK * 64 / 2;  // u32 [13][64/P+1] per-system counters
+    static constexpr uint32_t HROWS = 13;
+    // arrival masks u32 [64] at MQM, tails (| count << 16 at the final tier) u32 [64] at MQT:
+    // one word per lane in each (publishing, exchanging: one bank per lane), and the pad
+    // puts a receiver's mask and tail in different banks (they are read together)
+    static constexpr uint32_t MQ = HST + HROWS * HSTRIDE;
+    static constexpr uint32_t MQM = MQ, MQT = MQ + 65, MQS = 1;
+    static constexpr uint32_t DUM = MQ + 129;               // u32 [64]      target of a suppressed store
     static constexpr uint32_t WORDS = DUM + (DASH_MASKED_STORE ? 0 : 64);
 };
 
@@ -157,7 +161,7 @@ void sim_kernel(const SimArgs a) {
 #pragma unroll
     for (uint32_t i = 0; i < ncs; ++i) lds16[L::CAC * 2 + i * 64 + sw] = 0xFFu;
     for (uint32_t w = lane; w < L::HROWS * L::HSTRIDE; w += 64) lds[L::HST + w] = 0u;
-    lds[L::MQ + 2 * lane] = 0u;
+    lds[L::MQM + L::MQS * lane] = 0u;
     char* const ldsb = reinterpret_cast<char*>(lds);
     constexpr uint32_t SLOT = 64 * 4;                 // bytes per ring slot (one word per lane)
     constexpr uint32_t RMASK = RING * SLOT - 1;       // RING is a power of two
@@ -307,8 +311,11 @@ void sim_kernel(const SimArgs a) {
         }
         // messages handled per transactionType, per system; a lane without a message counts
         // into the unused row 13, so no exec mask is needed
-        __hip_atomic_fetch_add(&lds[L::HST + pty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        // messages handled per transactionType, per system (exec-masked: a dummy row for the
+        // lanes without a message measured 4 points more LDS bank conflicts, same time)
+        if (B(mHas))
+            __hip_atomic_fetch_add(&lds[L::HST + mty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
 
 #if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU)  // issue-cost probes (tools/ only)
         {
@@ -440,22 +447,23 @@ void sim_kernel(const SimArgs a) {
         // bits below its own, and the receiver's capacity check (ref :754-761)
         // compares the receiver's count plus that rank with the ring depth.
         // tail (with ring column); the final tier adds count << 16 for the capacity check
-        lds[L::MQ + 2 * lane + 1] = FINAL ? tq | (cq << 8) : tq;
+        lds[L::MQT + L::MQS * lane] = FINAL ? tq | (cq << 8) : tq;
         const uint32_t bitP = bitI << 1, bitB = bitI << 2;
         if (B(mVP))
-            __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (B(mVB))
-            __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         // REPLY_ID's INV fan-out (ref :364-373), ascending receivers: a wave-uniform test
         // guards each of its loops (arrival bits here, ring stores after the other sends)
         if (mRID != 0 && B(mRID)) {
             COLD();
             for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
-                __hip_atomic_fetch_or(&lds[L::MQ + 2 * (seg + (uint32_t)__builtin_ctz(im))], bitI,
+                __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + (uint32_t)__builtin_ctz(im))], bitI,
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         auto place = [&](mask_t v, uint32_t d, uint32_t bit, uint32_t w) {
-            const uint2 q = *reinterpret_cast<const uint2*>(&lds[L::MQ + 2 * (seg + d)]);
+            const uint32_t rcv = L::MQS * (seg + d);
+            const uint2 q = make_uint2(lds[L::MQM + rcv], lds[L::MQT + rcv]);
             const uint32_t rank = (uint32_t)__builtin_popcount(q.x & (bit - 1u));
             // slot byte offset = receiver tail + rank slots, in the receiver's ring
             // column (bits 7..2, untouched by the add); the count bits above bit 15
@@ -481,7 +489,7 @@ void sim_kernel(const SimArgs a) {
             for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
                 place(M(true), (uint32_t)__builtin_ctz(im), bitI, winv);
         }
-        const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQ + 2 * lane], 0u, __ATOMIC_RELAXED,
+        const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQM + L::MQS * lane], 0u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         uint32_t n = (uint32_t)__builtin_popcount(arrived) << 8;
         if constexpr (FINAL) n = min(n, RING * SLOT - cq);  // sendMessage's drop (ref :754-761)

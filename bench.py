@@ -263,6 +263,16 @@ def sweep(args, dash, rank, world, dev):
         dist.destroy_process_group()
 
 
+def host_trace_batch(seed, M, L):
+    """The --host-traces workload: [M][8][L] packed u16 words from numpy's PCG64 raw bits
+    (uniform-like over nodes, blocks, R/W and values); RD words keep their random value bits,
+    which the library ignores (ref :839, dash.h). Also used by tests/test_gpu_host_path.py."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    packed = rng.bit_generator.random_raw(M * 8 * L // 4).view(np.uint16).reshape(M, 8, L)
+    return packed, np.full((M, 8), L, dtype=np.uint32)
+
+
 def host_traces(args, dash, rank, world, dev):
     """PCIe-inclusive rate of the host-buffer boundary: per step, dash_load_traces (one strided
     H2D copy of the caller's [system][node][instr] u16 array) plus the run. Synthetic uniform
@@ -275,13 +285,7 @@ def host_traces(args, dash, rank, world, dev):
     import torch
     import torch.distributed as dist
     M, L = args.systems, args.len
-    rng = np.random.default_rng(args.seed + rank)
-    packed = rng.bit_generator.random_raw(M * 8 * L // 4).view(np.uint16).reshape(M, 8, L)
-    flat = packed.reshape(-1)
-    for i in range(0, flat.size, 1 << 26):  # RD carries value 0 (ref :839)
-        blk = flat[i:i + (1 << 26)]
-        blk &= (blk >> 15) * np.uint16(0xFF) | np.uint16(0xFF00)
-    lens = np.full((M, 8), L, dtype=np.uint32)
+    packed, lens = host_trace_batch(args.seed + rank, M, L)
     B = args.host_batches
     if B < 1 or M % B:
         raise SystemExit("--host-batches must divide --systems")

@@ -180,7 +180,7 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     chk(hipEventCreate(&h->ev1), "hipEventCreate");
     const uint64_t nsys = cfg->num_systems;
     const uint64_t trace_words = h->groups * (uint64_t)std::max<uint32_t>(h->nchunks, 1) * 64;
-    chk(hipMalloc(&h->d_trace, trace_words * sizeof(uint2)), "hipMalloc(trace)");
+    chk(hipMalloc(&h->d_trace, (trace_words + dash::TRACE_PAD) * sizeof(uint2)), "hipMalloc(trace)");
     chk(hipMalloc(&h->d_lens, std::max<uint64_t>(nsys * N, 1) * sizeof(uint32_t)), "hipMalloc(lens)");
     chk(hipMalloc(&h->d_digests, std::max<uint64_t>(nsys, 1) * sizeof(uint64_t)), "hipMalloc(digests)");
     chk(hipMalloc(&h->d_rounds, std::max<uint64_t>(nsys, 1) * sizeof(uint32_t)), "hipMalloc(rounds)");

@@ -79,6 +79,9 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring
 constexpr int NUM_TIERS = 3;
 constexpr uint32_t RING_TIERS[NUM_TIERS] = {16, 32, 256};
 constexpr uint32_t CHUNK_INSTR = 4;  // instructions per 8-B trace chunk
+// spare 8-B chunks after the trace buffer: a lane's window refill reads up to two chunks past
+// its last instruction (never issued), so the last lane's stream needs no bounds test
+constexpr uint64_t TRACE_PAD = 64;
 hipError_t launch_gen(const GenArgs& g, hipStream_t s);
 // skip[list[i]] = 1 for i < n
 // RD words carry value 0 (ref :839): clears bits 7..0 of every word whose bit 15 is 0

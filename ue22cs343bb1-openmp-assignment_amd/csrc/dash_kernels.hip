@@ -173,7 +173,9 @@ void sim_kernel(const SimArgs a) {
     // one lane's stream is contiguous (layout unit: 8-B chunks of 4), read in WCHUNK pieces
     const wchunk_t* tr = reinterpret_cast<const wchunk_t*>(
         a.trace + ((sys / SPW) * 64 + (sys % SPW) * P + t) * a.nchunks);
-    const uint32_t nch = (len + WCHUNK - 1) / WCHUNK;
+    // Chunks past a node's last instruction are read too (never issued: the pc < len guard);
+    // the trace buffer carries TRACE_PAD spare chunks after the last lane's stream, so no
+    // refill needs a bounds test
     // instruction i of a lane lives in window row i % (WIN*WCHUNK)
     auto put_chunk = [&](uint32_t c, wchunk_t v) {
         uint16_t* const w = lds16 + L::WND * 2 + ((c % WIN) * WCHUNK) * 64 + sw;
@@ -188,10 +190,10 @@ void sim_kernel(const SimArgs a) {
     };
 #pragma unroll
     for (uint32_t c = 0; c < WIN; ++c)
-        if (c < nch) put_chunk(c, tr[c]);
+        put_chunk(c, tr[c]);
     uint32_t pend_idx = WIN;
     wchunk_t pend{};
-    if (pend_idx < nch) pend = tr[pend_idx];
+    pend = tr[pend_idx];
 
     // this node's incoming queue (messageBuffer, ref :81-87): tail and count of
     // its LDS ring in ring-slot bytes (x SLOT), owned by the node; senders learn
@@ -549,10 +551,10 @@ void sim_kernel(const SimArgs a) {
         // holds chunks pend_idx-2 and pend_idx-1. pc advances <= WCHUNK per WCHUNK rounds,
         // so the chunks read until the next refill point (pc/WCHUNK, pc/WCHUNK + 1) are
         // always resident; the pending chunk's load has WCHUNK rounds to land.
-        if (pend_idx < nch && pend_idx < pc / (WCHUNK * PCU) + WIN) {
+        if (pend_idx < pc / (WCHUNK * PCU) + WIN) {
             put_chunk(pend_idx, pend);
             ++pend_idx;
-            if (pend_idx < nch) pend = tr[pend_idx];
+            pend = tr[pend_idx];
         }
         step(0, mMsg, mIss);
 #pragma unroll

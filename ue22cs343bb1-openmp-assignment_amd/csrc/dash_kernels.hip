@@ -53,7 +53,7 @@ constexpr uint32_t WCHUNK = DASH_WCHUNK;  // instructions per window refill (2: 
 static_assert(WCHUNK == 2 || WCHUNK == 4, "window chunk");
 using wchunk_t = typename std::conditional<WCHUNK == 4, uint2, uint32_t>::type;
 #ifndef DASH_QCHECK
-#define DASH_QCHECK 4              // rounds between quiescence votes (= WCHUNK: one trip of the round loop)
+#define DASH_QCHECK 4              // rounds between quiescence votes: one trip of the round loop (WCHUNK or 2 x WCHUNK)
 #endif
 #ifndef DASH_MASKED_STORE
 #define DASH_MASKED_STORE 0
@@ -191,9 +191,7 @@ void sim_kernel(const SimArgs a) {
 #pragma unroll
     for (uint32_t c = 0; c < WIN; ++c)
         put_chunk(c, tr[c]);
-    uint32_t pend_idx = WIN;
-    wchunk_t pend{};
-    pend = tr[pend_idx];
+    wchunk_t pend = tr[WIN];
 
     // this node's incoming queue (messageBuffer, ref :81-87): tail and count of
     // its LDS ring in ring-slot bytes (x SLOT), owned by the node; senders learn
@@ -204,6 +202,12 @@ void sim_kernel(const SimArgs a) {
     // the window address of the next instruction is one and-or
     constexpr uint32_t PCU = 128;
     uint32_t pc = 0, last_val = 0, lenx = len * PCU;
+    static_assert(WIN == 2, "window row of the pending chunk from rth");
+    // refill point: the pending chunk (index rth / CB + 1) lands once pc reaches rth, in
+    // window row ((rth + CB) & CB); pp points at it in HBM
+    constexpr uint32_t CB = WCHUNK * PCU;
+    uint32_t rth = CB;
+    const wchunk_t* pp = tr + WIN;
     // waitingForReply (ref :157) of every lane as one wave mask: updated by the scalar
     // unit, read per lane through inverse_ballot (no VALU)
     uint64_t wmask = 0;
@@ -243,7 +247,7 @@ void sim_kernel(const SimArgs a) {
     uint32_t rv = 0;
     asm volatile("" : "+v"(rv));
     const uint32_t sw2 = sw * 2u;  // byte offset of this lane's u16 in a 128-B row
-#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU)
+#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU) || defined(DASH_PAD_VHALF)
     uint32_t padv[4] = {lane, lane + 1, lane + 2, lane + 3}, pads[4] = {0, 1, 2, 3};
 #endif
 
@@ -284,9 +288,10 @@ void sim_kernel(const SimArgs a) {
         // message addresses are < 0x80 (a send to a node >= N is dropped), so bits
         // 14..8 give the address of a message and of an instruction alike
         const uint32_t mw = B(mHas) ? m : ins;
-        const uint32_t addr = (mw >> 8) & 0x7Fu;
+        uint32_t addr;  // (mw >> 8) & 0x7F as one bfe (the selector would split it into a shift and an and)
+        asm("v_bfe_u32 %0, %1, 8, 7" : "=v"(addr) : "v"(mw));
         const uint32_t b = addr & 15u;
-        const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
+        const uint32_t H = (mw >> 12) & 7u;  // procNodeAddr (ref :186, :657); one bfe, like addr
         // cacheIndex = blockIndex % CACHE_SIZE (ref :188)
         const uint32_t idx = CS ? b % (uint32_t)CS : (uint32_t)(a.cs_lut >> (4 * b)) & 15u;
         // byte offsets of the row entries; they stay in VGPRs from the loads to the stores
@@ -319,8 +324,12 @@ void sim_kernel(const SimArgs a) {
             __hip_atomic_fetch_add(&lds[L::HST + mty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
 
-#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU)  // issue-cost probes (tools/ only)
+#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU) || defined(DASH_PAD_VHALF)  // issue-cost probes (tools/ only)
         {
+#ifdef DASH_PAD_VHALF  // 3-operand VALU (v_bfe_u32: 4 cycles per wave64 on a SIMD in tools/micro/valu_ops)
+            asm volatile(".rept %4\n v_bfe_u32 %0, %0, 1, 30\n v_bfe_u32 %1, %1, 1, 30\n v_bfe_u32 %2, %2, 1, 30\n v_bfe_u32 %3, %3, 1, 30\n .endr"
+                         : "+v"(padv[0]), "+v"(padv[1]), "+v"(padv[2]), "+v"(padv[3]) : "i"(DASH_PAD_VHALF / 4));
+#endif
 #ifdef DASH_PAD_VALU
             asm volatile(".rept %4\n v_add_u32 %0, 1, %0\n v_add_u32 %1, 1, %1\n v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n .endr"
                          : "+v"(padv[0]), "+v"(padv[1]), "+v"(padv[2]), "+v"(padv[3]) : "i"(DASH_PAD_VALU / 4));
@@ -435,7 +444,10 @@ void sim_kernel(const SimArgs a) {
         }
 
         *ent = (uint16_t)(nmem | (nbv << 8));
-        *cac = (uint16_t)(B(mFill) ? (addr | (fval << 8)) : c16);
+        // the select stays 32-bit (an i16 select would make the line load's zero extension an AND)
+        uint32_t cw = B(mFill) ? (addr | (fval << 8)) : c16;
+        asm volatile("" : "+v"(cw));
+        *cac = (uint16_t)cw;
         dsv = (dsv & ~(3u << (2 * b))) | (nds << (2 * b));
         cst = (cst & ~(3u << (2 * idx))) | (nst << (2 * idx));
 
@@ -455,14 +467,6 @@ void sim_kernel(const SimArgs a) {
             __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (B(mVB))
             __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        // REPLY_ID's INV fan-out (ref :364-373), ascending receivers: a wave-uniform test
-        // guards each of its loops (arrival bits here, ring stores after the other sends)
-        if (mRID != 0 && B(mRID)) {
-            COLD();
-            for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
-                __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + (uint32_t)__builtin_ctz(im))], bitI,
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
         auto place = [&](mask_t v, uint32_t d, uint32_t bit, uint32_t w) {
             const uint32_t rcv = L::MQS * (seg + d);
             const uint2 q = make_uint2(lds[L::MQM + rcv], lds[L::MQT + rcv]);
@@ -483,14 +487,25 @@ void sim_kernel(const SimArgs a) {
                 if (B(v)) *reinterpret_cast<uint32_t*>(ldsb + L::RNG * 4 + off) = w;
             }
         };
+        // REPLY_ID's INV fan-out (ref :364-373), ascending receivers, behind one wave-uniform
+        // test: its arrival bits, then its ring stores. The primary and flush-copy bits are
+        // already set above, so these ranks see every arrival of the round; the places below
+        // read the masks after the INV bits too.
+        if (mRID != 0) {
+            COLD();
+            if (B(mRID)) {
+                for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
+                    __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + (uint32_t)__builtin_ctz(im))], bitI,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (B(mRID)) {
+                const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
+                for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
+                    place(M(true), (uint32_t)__builtin_ctz(im), bitI, winv);
+            }
+        }
         place(mVP, dP, bitP, wP);
         place(mVB, msr, bitB, wA);
-        if (mRID != 0 && B(mRID)) {
-            COLD();
-            const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
-            for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
-                place(M(true), (uint32_t)__builtin_ctz(im), bitI, winv);
-        }
         const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQM + L::MQS * lane], 0u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         uint32_t n = (uint32_t)__builtin_popcount(arrived) << 8;
@@ -507,17 +522,10 @@ void sim_kernel(const SimArgs a) {
         maxd = max(maxd, cq);
     };
 
-    // WCHUNK rounds per trip, unrolled; the trip's start is the housekeeping point
-    // (quiescence vote, round cap, overflow stop, trace window refill)
-    static_assert(DASH_QCHECK == WCHUNK, "one housekeeping point per WCHUNK rounds");
-    for (;; rv += WCHUNK) {
-        mask_t mMsg = can_pop(), mIss = can_issue();
-        // quiescence is absorbing, so testing it once per trip only adds idle rounds (no
-        // state changes, not counted in `rounds`)
-        if ((mMsg | mIss) == 0) break;
-        // the round cap is a multiple of WCHUNK (dash_create rounds it up), so it can only
-        // fall on a trip's first round
-        if (M(rv == cap) != 0) {  // wave-uniform: every system still active has run `cap` rounds
+    // the round cap is a multiple of WCHUNK (dash_create rounds it up), so it can only
+    // fall on the first round of a WCHUNK block
+    auto cap_check = [&](const uint32_t r0, mask_t& mMsg, mask_t& mIss) __attribute__((always_inline)) {
+        if (M(r0 == cap) != 0) {  // wave-uniform: every system still active has run `cap` rounds
             COLD();
             const bool kill = ((uint32_t)((mMsg | mIss) >> seg) & SEGMASK) != 0;
             const mask_t mKill = M(kill);
@@ -530,6 +538,36 @@ void sim_kernel(const SimArgs a) {
                 lenx = pc;
             }
         }
+    };
+    // trace window refill. Invariant here: the window holds the two chunks before the
+    // pending one, and pc advances <= WCHUNK per WCHUNK rounds, so the chunks read until the
+    // next refill point are always resident; the pending chunk's load has WCHUNK rounds to land.
+    auto refill = [&]() __attribute__((always_inline)) {
+        if (pc >= rth) {
+            rth += CB;
+            uint16_t* const w = reinterpret_cast<uint16_t*>(ldsb + L::WND * 4 + ((rth & CB) | sw2));
+            uint32_t x, y;
+            chunk_words(pend, x, y);
+            w[0] = (uint16_t)x;
+            w[64] = (uint16_t)(x >> 16);
+            if constexpr (WCHUNK == 4) {
+                w[128] = (uint16_t)y;
+                w[192] = (uint16_t)(y >> 16);
+            }
+            pend = *++pp;
+        }
+    };
+
+    // TRIP rounds per trip of WCHUNK-round blocks, unrolled; the trip's start is the
+    // housekeeping point (quiescence vote, overflow stop), each block's start the round-cap
+    // test and the trace window refill
+    constexpr uint32_t TRIP = DASH_QCHECK;
+    static_assert(TRIP == WCHUNK || TRIP == 2 * WCHUNK, "one or two refill blocks per trip");
+    mask_t mMsg = can_pop(), mIss = can_issue();
+    // quiescence is absorbing, so testing it once per trip only adds idle rounds (no
+    // state changes, not counted in `rounds`)
+    while ((mMsg | mIss) != 0) {
+        cap_check(rv, mMsg, mIss);
         // a non-final tier stops a system soon after its first overflow: it will be
         // re-simulated from scratch at the next depth, its results here are void
         if (!FINAL) {
@@ -547,18 +585,22 @@ void sim_kernel(const SimArgs a) {
                 }
             }
         }
-        // trace window refill. Invariant here: pend_idx >= pc/WCHUNK + 1 and the window
-        // holds chunks pend_idx-2 and pend_idx-1. pc advances <= WCHUNK per WCHUNK rounds,
-        // so the chunks read until the next refill point (pc/WCHUNK, pc/WCHUNK + 1) are
-        // always resident; the pending chunk's load has WCHUNK rounds to land.
-        if (pend_idx < pc / (WCHUNK * PCU) + WIN) {
-            put_chunk(pend_idx, pend);
-            ++pend_idx;
-            pend = tr[pend_idx];
-        }
+        refill();
         step(0, mMsg, mIss);
 #pragma unroll
         for (uint32_t k = 1; k < WCHUNK; ++k) step(k, can_pop(), can_issue());
+        if constexpr (TRIP == 2 * WCHUNK) {
+            mMsg = can_pop();
+            mIss = can_issue();
+            cap_check(rv + WCHUNK, mMsg, mIss);
+            refill();
+            step(WCHUNK, mMsg, mIss);
+#pragma unroll
+            for (uint32_t k = WCHUNK + 1; k < TRIP; ++k) step(k, can_pop(), can_issue());
+        }
+        rv += TRIP;
+        mMsg = can_pop();
+        mIss = can_issue();
     }
 
     // ---- results ----

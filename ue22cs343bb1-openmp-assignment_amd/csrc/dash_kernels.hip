@@ -55,9 +55,6 @@ using wchunk_t = typename std::conditional<WCHUNK == 4, uint2, uint32_t>::type;
 #ifndef DASH_QCHECK
 #define DASH_QCHECK 4              // rounds between quiescence votes: one trip of the round loop (WCHUNK or 2 x WCHUNK)
 #endif
-#ifndef DASH_MASKED_STORE
-#define DASH_MASKED_STORE 0
-#endif
 #ifndef DASH_WAVES_PER_EU
 #define DASH_WAVES_PER_EU 0
 #endif
@@ -86,20 +83,21 @@ constexpr int cs_rows() { return CS ? CS : 16; }
 
 template <int P, int CS, uint32_t RING>
 struct Lds {  // 32-bit word offsets
-    static constexpr uint32_t ENT = 0;                      // u16 [16][64]  mem | bitVector<<8   (swizzled)
+    // arrival masks u32 [64] at MQM, tails (| count << 16 at the final tier) u32 [64] at MQT:
+    // one word per lane in each (publishing, exchanging: one bank per lane), and the pad
+    // puts a receiver's mask and tail in different banks (they are read together, by one
+    // ds_read2 whose 8-bit offsets reach them from the receiver's address with no base add:
+    // hence at the bottom of the LDS)
+    static constexpr uint32_t MQ = 0;
+    static constexpr uint32_t MQM = MQ, MQT = MQ + 65, MQS = 1;
+    static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
+    static constexpr uint32_t HST = MQ + 129;               // u32 [13][64/P+1] per-system counters
+    static constexpr uint32_t HROWS = 13;
+    static constexpr uint32_t ENT = HST + HROWS * HSTRIDE;  // u16 [16][64]  mem | bitVector<<8   (swizzled)
     static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8      (swizzled)
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
-    static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
-    static constexpr uint32_t HST = WND + WIN * WCHUNK * 64 / 2;  // u32 [13][64/P+1] per-system counters
-    static constexpr uint32_t HROWS = 13;
-    // arrival masks u32 [64] at MQM, tails (| count << 16 at the final tier) u32 [64] at MQT:
-    // one word per lane in each (publishing, exchanging: one bank per lane), and the pad
-    // puts a receiver's mask and tail in different banks (they are read together)
-    static constexpr uint32_t MQ = HST + HROWS * HSTRIDE;
-    static constexpr uint32_t MQM = MQ, MQT = MQ + 65, MQS = 1;
-    static constexpr uint32_t DUM = MQ + 129;               // u32 [64]      target of a suppressed store
-    static constexpr uint32_t WORDS = DUM + (DASH_MASKED_STORE ? 0 : 64);
+    static constexpr uint32_t WORDS = WND + WIN * WCHUNK * 64 / 2;
 };
 
 __device__ __forceinline__ void chunk_words(uint2 v, uint32_t& x, uint32_t& y) { x = v.x; y = v.y; }

@@ -132,7 +132,8 @@ typedef struct dash_gen {
 
 /* One logged step of one node (cfg.trace_events > 0), in lockstep order. */
 #define DASH_EV_MSG 0u   /* handled a message: word = message word (type[3:0], sender[6:4],
-                            address[15:8], value|bitVector[23:16], secondReceiver[26:24]) */
+                            address[14:8], value|bitVector[23:16], secondReceiver[26:24];
+                            the other bits are zero) */
 #define DASH_EV_INSTR 1u /* issued an instruction: word = packed instruction */
 typedef struct dash_event {
     uint32_t round;

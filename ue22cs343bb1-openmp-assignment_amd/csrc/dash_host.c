@@ -185,7 +185,7 @@ int dash_format_event(const dash_event *e, char *buf, size_t cap) {
     int n;
     if (e->kind == DASH_EV_MSG) /* DEBUG_MSG (ref :180-181) */
         n = snprintf(buf, cap, "Processor %u msg from: %u, type: %u, address: 0x%02X\n", e->node,
-                     (e->word >> 4) & 7u, e->word & 15u, (e->word >> 8) & 0xFFu);
+                     (e->word >> 4) & 7u, e->word & 15u, (e->word >> 8) & 0x7Fu);
     else if (e->kind == DASH_EV_INSTR) /* DEBUG_INSTR (ref :650-651) */
         n = snprintf(buf, cap, "Processor %u: instr type=%c, address=0x%02X, value=%u\n", e->node,
                      (e->word & 0x8000u) ? 'W' : 'R', (e->word >> 8) & 0x7Fu, e->word & 0xFFu);

@@ -60,11 +60,12 @@ using wchunk_t = typename std::conditional<WCHUNK == 4, uint2, uint32_t>::type;
 #endif
 
 // message word (ref `message`, :70-79, 20 B -> 4 B):
-//   [3:0] type  [6:4] sender  [15:8] address  [23:16] value | bitVector
-//   [26:24] secondReceiver  [27] dirState == S
+//   [3:0] type  [6:4] sender  [7] dirState == S (REPLY_RD)  [14:8] address
+//   [15] the sender's reply-table flag (ignored)  [23:16] value | bitVector
+//   [26:24] secondReceiver  [31:27] zero (secondReceiver is one shift, no field extract)
 __device__ __forceinline__ uint32_t mk(uint32_t type, uint32_t sender, uint32_t addr,
                                        uint32_t val, uint32_t sr, uint32_t ds_s) {
-    return type | (sender << 4) | (addr << 8) | (val << 16) | (sr << 24) | (ds_s << 27);
+    return type | (sender << 4) | (ds_s << 7) | (addr << 8) | (val << 16) | (sr << 24);
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
@@ -109,6 +110,18 @@ using mask_t = uint64_t;
 __device__ __forceinline__ mask_t M(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 __device__ __forceinline__ bool B(mask_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 __device__ __forceinline__ uint64_t vote(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+// bit 7 / bit 15 of a lane value as a lane mask: one SDWA compare of the sign-extended low
+// byte / half word (the selector would otherwise extract the bit first)
+__device__ __forceinline__ mask_t Mbit7(uint32_t v) {
+    mask_t r;
+    asm("v_cmp_gt_i32_sdwa %0, 0, sext(%1) src0_sel:DWORD src1_sel:BYTE_0" : "=s"(r) : "v"(v));
+    return r;
+}
+__device__ __forceinline__ mask_t Mbit15(uint32_t v) {
+    mask_t r;
+    asm("v_cmp_gt_i32_sdwa %0, 0, sext(%1) src0_sel:DWORD src1_sel:WORD_0" : "=s"(r) : "v"(v));
+    return r;
+}
 // keeps a rarely taken branch a branch (no if-conversion onto the common path)
 #define COLD() asm volatile("" ::: "memory")
 
@@ -196,15 +209,17 @@ void sim_kernel(const SimArgs a) {
     // them through MQ each round. Below the final depth the count is not clamped:
     // exceeding RING is the overflow that hands the system to the next depth.
     uint32_t cq = 0, tq = lane * 4u;  // tail carries this node's ring column (bits below the slot)
-    // program counter and trace length pre-scaled by the window row stride (128 B), so
-    // the window address of the next instruction is one and-or
+    // program counter and trace length pre-scaled by the window row stride (128 B) and
+    // offset by this lane's byte in a row (< 128), so the window address of the next
+    // instruction is one and; pc / PCU is the instruction count
     constexpr uint32_t PCU = 128;
-    uint32_t pc = 0, last_val = 0, lenx = len * PCU;
+    const uint32_t sw2 = sw * 2u;  // byte offset of this lane's u16 in a 128-B row
+    uint32_t pc = sw2, last_val = 0, lenx = len * PCU + sw2;
     static_assert(WIN == 2, "window row of the pending chunk from rth");
     // refill point: the pending chunk (index rth / CB + 1) lands once pc reaches rth, in
     // window row ((rth + CB) & CB); pp points at it in HBM
     constexpr uint32_t CB = WCHUNK * PCU;
-    uint32_t rth = CB;
+    uint32_t rth = CB + sw2;
     const wchunk_t* pp = tr + WIN;
     // waitingForReply (ref :157) of every lane as one wave mask: updated by the scalar
     // unit, read per lane through inverse_ballot (no VALU)
@@ -221,14 +236,14 @@ void sim_kernel(const SimArgs a) {
     // reply table, one entry per lane, read with ds_bpermute: entry (step type s, dir state
     // d) at lane 4s + d. Step types: the message types, 13 = no step, 14 / 15 = issue RD / WR.
     // Bits 3..0: the reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue:
-    // :666-734); bit 27: REPLY_RD's dirState == S; bit 31 (SENDS): the step sends that reply,
-    // subject to the per-lane conditions applied after the lookup (ctz(0), hits). Receivers
-    // ignore bits 28..31 of a message word.
-    constexpr uint32_t SENDS = 1u << 31;
+    // :666-734); bit 7: REPLY_RD's dirState == S; bit 15 (SENDS): the step sends that reply,
+    // subject to the per-lane conditions applied after the lookup (ctz(0), hits). The flag
+    // travels in bit 15 of the message word, which receivers ignore (addresses are 7 bits).
+    constexpr uint32_t SENDS = 1u << 15;
     const uint32_t tatab = [&] {
         const uint32_t st = lane >> 2, d = lane & 3;
         switch (st) {
-        case T_RR: return SENDS | (d == D_EM ? (uint32_t)T_WBINT : (uint32_t)T_RRD | (d == D_S ? 1u << 27 : 0u));
+        case T_RR: return SENDS | (d == D_EM ? (uint32_t)T_WBINT : (uint32_t)T_RRD | (d == D_S ? 1u << 7 : 0u));
         case T_WRQ: return SENDS | (d == D_EM ? (uint32_t)T_WBINV : (d == D_S ? (uint32_t)T_RID : (uint32_t)T_RWR));
         case T_UPG: return SENDS | (uint32_t)T_RID;
         case T_WBINV: return SENDS | (uint32_t)T_FIA;
@@ -244,7 +259,6 @@ void sim_kernel(const SimArgs a) {
     // the trip's first step; the step at position k of the trip is round rv + k
     uint32_t rv = 0;
     asm volatile("" : "+v"(rv));
-    const uint32_t sw2 = sw * 2u;  // byte offset of this lane's u16 in a 128-B row
 #if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU) || defined(DASH_PAD_VHALF)
     uint32_t padv[4] = {lane, lane + 1, lane + 2, lane + 3}, pads[4] = {0, 1, 2, 3};
 #endif
@@ -277,7 +291,7 @@ void sim_kernel(const SimArgs a) {
         const mask_t mHas = mMsg & ~mStall;           // pops this round
         const mask_t mDo = mIss & ~mMsg & ~mStall;    // issues this round
         const uint32_t m = *reinterpret_cast<const uint32_t*>(ldsb + L::RNG * 4 + ((tq - cq) & RMASK));
-        const uint32_t ins = *reinterpret_cast<const uint16_t*>(ldsb + L::WND * 4 + ((pc & (WIN * WCHUNK * PCU - 1)) | sw2));
+        const uint32_t ins = *reinterpret_cast<const uint16_t*>(ldsb + L::WND * 4 + (pc & (WIN * WCHUNK * PCU - 1)));
         pc += B(mDo) ? PCU : 0u;
         if constexpr (SLOW || FINAL)
             cq -= B(mHas) ? SLOT : 0u;
@@ -352,7 +366,7 @@ void sim_kernel(const SimArgs a) {
         const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
         const uint32_t laddr = c16 & 0xFFu, lval = c16 >> 8, lst = (cst >> (2 * idx)) & 3u;
         const uint32_t msender = (m >> 4) & 7u, mval = (mw >> 16) & 0xFFu;
-        const uint32_t msr = (m >> 24) & 7u;
+        const uint32_t msr = m >> 24;  // bits 31..27 are zero
         const uint32_t ival = ins & 0xFFu;
         const uint32_t sbit = 1u << msender;
 
@@ -392,7 +406,7 @@ void sim_kernel(const SimArgs a) {
         // a WR hit with its own (= the new last value)
         last_val = B(mDo) ? ival : last_val;
         const uint32_t fval = B(mRRD | mFLUSH) ? mval : last_val;
-        const mask_t mDsS = M((m & (1u << 27)) != 0);     // REPLY_RD's dirState == S
+        const mask_t mDsS = Mbit7(m);                      // REPLY_RD's dirState == S (bit 7)
         const mask_t mOwnHome = M(es_own == H);
         const mask_t mToI = (mINV & mSame) | mWBINV;                                   // :396-398 :501
         const mask_t mToS = mWBINT | (mRRD & mDsS) | (mFLUSH & mtSR);                  // :284 :252 :319
@@ -409,7 +423,7 @@ void sim_kernel(const SimArgs a) {
         // notice -- no handler sends both (fills never reply), so one slot serves both
         uint32_t tA = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sty << 4) | (ds << 2)), (int)tatab);
         // a hit needs no request (:676-677, :706-710), except a WR hit on SHARED (UPGRADE)
-        const mask_t mVA = (M((int32_t)tA < 0) & ~mCtz0 & ~((miR & mHit) | mOwnHit)) | (mEsOne & ~mOwnHome);
+        const mask_t mVA = (Mbit15(tA) & ~mCtz0 & ~((miR & mHit) | mOwnHit)) | (mEsOne & ~mOwnHome);
         uint32_t dA = B(mReq | mUPG) ? msender : H;
         dA = B(mEmReq) ? (uint32_t)__builtin_ctz(bv | 0x100u) : dA;
         dA = B(mEsH) ? es_own : dA;

@@ -41,7 +41,7 @@ enum : uint32_t {
     T_WBINV = 7, T_WBINT = 8, T_FLUSH = 9, T_FIA = 10, T_ES = 11, T_EMOD = 12,
     T_ISSUE_R = 13, T_ISSUE_W = 14, T_IDLE = 15
 };
-enum : uint32_t { ST_M = 0, ST_E = 1, ST_S = 2, ST_I = 3 };  // cacheLineState (ref :17)
+enum : uint32_t { ST_M = 0, ST_E = 1, ST_S = 2, ST_I = 3 };  // cacheLineState (ref :17); evb needs ST_M = 0
 enum : uint32_t { D_EM = 0, D_S = 1, D_U = 2 };              // directoryEntryState (ref :28)
 
 #ifndef DASH_WCHUNK
@@ -112,6 +112,12 @@ __device__ __forceinline__ bool B(mask_t m) { return __builtin_amdgcn_inverse_ba
 __device__ __forceinline__ uint64_t vote(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 // bit 7 / bit 15 of a lane value as a lane mask: one SDWA compare of the sign-extended low
 // byte / half word (the selector would otherwise extract the bit first)
+// index of the lowest set bit, all ones for 0 (v_ffbl_b32; the callers never use the 0 case)
+__device__ __forceinline__ uint32_t ffbl(uint32_t v) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
 __device__ __forceinline__ mask_t Mbit7(uint32_t v) {
     mask_t r;
     asm("v_cmp_gt_i32_sdwa %0, 0, sext(%1) src0_sel:DWORD src1_sel:BYTE_0" : "=s"(r) : "v"(v));
@@ -232,7 +238,9 @@ void sim_kernel(const SimArgs a) {
     uint32_t cap = a.max_rounds, nlim = N * 16u, rcv_all = rcv_mask;
     asm volatile("" : "+v"(cap), "+v"(nlim), "+v"(rcv_all));
 
-    const uint32_t wES = T_ES | (t << 4), wEM = T_EMOD | (t << 4);  // eviction notice, sender part
+    // eviction notice (ref :767-804), sender part by the line state: EVICT_MODIFIED for M,
+    // EVICT_SHARED otherwise; byte k of evb is the first message byte for line state k
+    const uint32_t evb = (T_EMOD | (t << 4)) | (T_ES | (t << 4)) * 0x01010100u;
     // reply table, one entry per lane, read with ds_bpermute: entry (step type s, dir state
     // d) at lane 4s + d. Step types: the message types, 13 = no step, 14 / 15 = issue RD / WR.
     // Bits 3..0: the reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue:
@@ -255,6 +263,22 @@ void sim_kernel(const SimArgs a) {
         }
     }();
 
+    // field source table, same index as the reply table: a v_perm selector that assembles
+    // bytes 1..3 of the reply (address, value field, secondReceiver; byte 0 zero). Pool bytes:
+    // 0..3 = mw (0: the issued value, 1: the address, 2: the message value, 3: the message's
+    // secondReceiver), 4 = memory, 5 = the line's value, 6 = sharers less sender, 7 = sender
+    const uint32_t vstab = [&] {
+        const uint32_t st = lane >> 2, d = lane & 3;
+        uint32_t src = 4u;                                           // memory (RR, ES, ...)
+        if (st == T_WBINV || st == T_WBINT) src = 5u;                // written-back line value
+        if (st == T_UPG || (st == T_WRQ && d != D_EM)) src = 6u;     // sharers to invalidate
+        if (st == T_WRQ && d == D_EM) src = 2u;                      // forwarded write value
+        if (st == 14 || st == 15) src = 0u;                          // issued value
+        // a forwarded request's reply passes its secondReceiver on (ref :281, :498); other
+        // sends name the message's sender (the requester, for a forward)
+        const uint32_t sr = (st == T_WBINV || st == T_WBINT) ? 3u : 7u;
+        return 0x0000010Cu | (src << 16) | (sr << 24);  // byte 0: 0x0C selects zero
+    }();
     // round counter: rv (a VGPR copy, so the lane masks keep the SGPRs) is the round of
     // the trip's first step; the step at position k of the trip is round rv + k
     uint32_t rv = 0;
@@ -364,20 +388,21 @@ void sim_kernel(const SimArgs a) {
         const mask_t miR = M(sty == 14u), miW = M(sty == 15u);
 
         const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
-        const uint32_t laddr = c16 & 0xFFu, lval = c16 >> 8, lst = (cst >> (2 * idx)) & 3u;
+        const uint32_t laddr = c16 & 0xFFu, lst = (cst >> (2 * idx)) & 3u;
         const uint32_t msender = (m >> 4) & 7u, mval = (mw >> 16) & 0xFFu;
         const uint32_t msr = m >> 24;  // bits 31..27 are zero
         const uint32_t ival = ins & 0xFFu;
         const uint32_t sbit = 1u << msender;
 
         const mask_t mEM = M(ds == D_EM), mS = M(ds == D_S), mU = ~(mEM | mS);
-        const mask_t mlI = M(lst == ST_I), mlS = M(lst == ST_S), mlM = M(lst == ST_M);
+        const mask_t mlI = M(lst == ST_I), mlS = M(lst == ST_S);
         const mask_t mtH = M(t == H), mtSR = M(t == msr), mSame = M(laddr == addr);
         const mask_t mHit = mSame & ~mlI;                 // ref :662-664
         const mask_t mOwnHit = miW & mHit & ~mlS;         // WR hit on M/E (:706-710)
         const uint32_t es_bv = bv & ~sbit;                // also UPGRADE/WRITE_REQUEST's sharer list
         const uint32_t es_pop = (uint32_t)__builtin_popcount(es_bv);
-        const uint32_t es_own = (uint32_t)__builtin_ctz(es_bv | 0x100u);  // meaningful when es_pop == 1
+        const uint32_t es_own = ffbl(es_bv);  // used only when es_pop == 1
+        const uint32_t own = ffbl(bv);        // the owner at EM (bv == 0 is mCtz0: dropped, unused)
         const mask_t mEsH = mES & mtH;
         const mask_t mEsOne = mEsH & M(es_pop == 1u);
         const mask_t mReq = mRR | mWRQ;
@@ -425,20 +450,19 @@ void sim_kernel(const SimArgs a) {
         // a hit needs no request (:676-677, :706-710), except a WR hit on SHARED (UPGRADE)
         const mask_t mVA = (Mbit15(tA) & ~mCtz0 & ~((miR & mHit) | mOwnHit)) | (mEsOne & ~mOwnHome);
         uint32_t dA = B(mReq | mUPG) ? msender : H;
-        dA = B(mEmReq) ? (uint32_t)__builtin_ctz(bv | 0x100u) : dA;
+        dA = B(mEmReq) ? own : dA;
         dA = B(mEsH) ? es_own : dA;
         // reply type (READ_REQUEST: ref :199-236, WRITE_REQUEST: :417-453, issue: :666-734);
         // REPLY_RD carries dirState == S in bit 27 (the other receivers ignore it)
         tA = B(miW & mHit) ? (uint32_t)T_UPG : tA;
-        uint32_t valA = B(mWBINV | mWBINT) ? lval : mem;
-        valA = B(mDo) ? ival : valA;
-        valA = B(mUPG | (mWRQ & ~mEM)) ? es_bv : valA;
-        valA = B(mWRQ & mEM) ? mval : valA;
-        const uint32_t srA = B(mWBINV | mWBINT) ? msr : msender;
-        const uint32_t wA = tA | (t << 4) | (mw & 0x7F00u) | (valA << 16) | (srA << 24);
+        const uint32_t vsel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sty << 4) | (ds << 2)), (int)vstab);
+        const uint32_t vpool = __builtin_amdgcn_perm(c16, e16, 0x0C0C0500u) | (es_bv << 16) | (msender << 24);
+        const uint32_t av16 = __builtin_amdgcn_perm(vpool, mw, vsel);  // address and value fields, in place
+        const uint32_t wA = tA | (t << 4) | av16;  // bit 15 of the address byte: ignored
         const uint32_t dE = laddr >> 4;
         const mask_t mInN = M(laddr < nlim);  // home node of the evicted line exists
-        const uint32_t wE = (B(mlM) ? wEM : wES) | (c16 << 8);
+        // one byte permute: [evb byte lst, line address, line value, 0]
+        const uint32_t wE = __builtin_amdgcn_perm(c16, evb, lst | 0x0C050400u);
         const mask_t mVP = mVA | (mEv & mInN);
         const uint32_t dP = B(mVA) ? dA : dE;
         const uint32_t wP = B(mVA) ? wA : wE;
@@ -456,7 +480,7 @@ void sim_kernel(const SimArgs a) {
         }
 
         *ent = (uint16_t)(nmem | (nbv << 8));
-        // the select stays 32-bit (an i16 select would make the line load's zero extension an AND)
+        // the select stays 32-bit (an i16 select costs more conversions)
         uint32_t cw = B(mFill) ? (addr | (fval << 8)) : c16;
         asm volatile("" : "+v"(cw));
         *cac = (uint16_t)cw;

@@ -92,8 +92,8 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t MQ = 0;
     static constexpr uint32_t MQM = MQ, MQT = MQ + 65, MQS = 1;
     static constexpr uint32_t HSTRIDE = 64 / P + 1;         // padded: a system's 13 rows hit 13 banks
-    static constexpr uint32_t HST = MQ + 129;               // u32 [13][64/P+1] per-system counters
-    static constexpr uint32_t HROWS = 13;
+    static constexpr uint32_t HST = MQ + 129;               // u32 [14][64/P+1] per-system counters
+    static constexpr uint32_t HROWS = 14;                   // 13 types + row 13: lanes that do not pop
     static constexpr uint32_t ENT = HST + HROWS * HSTRIDE;  // u16 [16][64]  mem | bitVector<<8   (swizzled)
     static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8      (swizzled)
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
@@ -327,7 +327,7 @@ void sim_kernel(const SimArgs a) {
         uint32_t addr;  // (mw >> 8) & 0x7F as one bfe (the selector would split it into a shift and an and)
         asm("v_bfe_u32 %0, %1, 8, 7" : "=v"(addr) : "v"(mw));
         const uint32_t b = addr & 15u;
-        const uint32_t H = (mw >> 12) & 7u;  // procNodeAddr (ref :186, :657); one bfe, like addr
+        const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
         // cacheIndex = blockIndex % CACHE_SIZE (ref :188)
         const uint32_t idx = CS ? b % (uint32_t)CS : (uint32_t)(a.cs_lut >> (4 * b)) & 15u;
         // byte offsets of the row entries; they stay in VGPRs from the loads to the stores
@@ -353,12 +353,10 @@ void sim_kernel(const SimArgs a) {
             }
         }
         // messages handled per transactionType, per system; a lane without a message counts
-        // into the unused row 13, so no exec mask is needed
-        // messages handled per transactionType, per system (exec-masked: a dummy row for the
-        // lanes without a message measured 4 points more LDS bank conflicts, same time)
-        if (B(mHas))
-            __hip_atomic_fetch_add(&lds[L::HST + mty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        // into row 13 (pty = 13), so no exec mask is needed (more LDS bank conflicts on that
+        // row, 22.6 -> 26.6 % of LDS cycles, but 1.7 % less kernel time than exec-masking)
+        __hip_atomic_fetch_add(&lds[L::HST + pty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
 
 #if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU) || defined(DASH_PAD_VHALF)  // issue-cost probes (tools/ only)
         {
@@ -387,11 +385,12 @@ void sim_kernel(const SimArgs a) {
         const uint32_t sty = B(mDo) ? (ins >> 15) | 14u : pty;  // step type: 14 / 15 = issue RD / WR
         const mask_t miR = M(sty == 14u), miW = M(sty == 15u);
 
-        const uint32_t mem = e16 & 0xFFu, bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
+        const uint32_t bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
         const uint32_t laddr = c16 & 0xFFu, lst = (cst >> (2 * idx)) & 3u;
-        const uint32_t msender = (m >> 4) & 7u, mval = (mw >> 16) & 0xFFu;
+        // the message's value field in bits 7..0 (secondReceiver above it: every consumer
+        // takes the low byte only -- a byte permute, a u16 store, an AND)
+        const uint32_t msender = (m >> 4) & 7u, mv16 = mw >> 16;
         const uint32_t msr = m >> 24;  // bits 31..27 are zero
-        const uint32_t ival = ins & 0xFFu;
         const uint32_t sbit = 1u << msender;
 
         const mask_t mEM = M(ds == D_EM), mS = M(ds == D_S), mU = ~(mEM | mS);
@@ -423,14 +422,16 @@ void sim_kernel(const SimArgs a) {
         uint32_t nds = B(mToReq | mEsOne) ? (uint32_t)D_EM : ds;
         nds = B(mFLUSH & mtH) ? (uint32_t)D_S : nds;
         nds = B(mEMOD | (mEsH & M(es_pop == 0u))) ? (uint32_t)D_U : nds;
-        const uint32_t nmem = B(mHomeH | mEMOD) ? mval : mem;  // :307 :520 :602
+        // memory takes the message's value (:307 :520 :602): the entry's byte 0 comes from
+        // the message word instead of the old entry
+        const uint32_t ebase = B(mHomeH | mEMOD) ? mv16 : e16;
 
         // cache line: the new state by the value it takes (the type sets are disjoint)
         const mask_t mFill = mRRD | mRWR | mRID | ((mFLUSH | mFIA) & mtSR) | mOwnHit;
         // REPLY_WR / REPLY_ID / FLUSH_INVACK fill with the last issued value (:470,383,531),
         // a WR hit with its own (= the new last value)
-        last_val = B(mDo) ? ival : last_val;
-        const uint32_t fval = B(mRRD | mFLUSH) ? mval : last_val;
+        last_val = B(mDo) ? ins : last_val;  // value in bits 7..0 (the address above it: dropped below)
+        const uint32_t fval = B(mRRD | mFLUSH) ? mv16 : last_val;
         const mask_t mDsS = Mbit7(m);                      // REPLY_RD's dirState == S (bit 7)
         const mask_t mOwnHome = M(es_own == H);
         const mask_t mToI = (mINV & mSame) | mWBINV;                                   // :396-398 :501
@@ -479,7 +480,7 @@ void sim_kernel(const SimArgs a) {
             drops += (B(mOob) ? 1u : 0u) + (B(mCtz0) ? 1u : 0u);
         }
 
-        *ent = (uint16_t)(nmem | (nbv << 8));
+        *ent = (uint16_t)__builtin_amdgcn_perm(nbv, ebase, 0x0C0C0400u);  // [memory, sharers]
         // the select stays 32-bit (an i16 select costs more conversions)
         uint32_t cw = B(mFill) ? (addr | (fval << 8)) : c16;
         asm volatile("" : "+v"(cw));
@@ -530,13 +531,13 @@ void sim_kernel(const SimArgs a) {
         if (mRID != 0) {
             COLD();
             if (B(mRID)) {
-                for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
+                for (uint32_t im = mv16 & rcv_all; im != 0; im &= im - 1u)
                     __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + (uint32_t)__builtin_ctz(im))], bitI,
                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             if (B(mRID)) {
                 const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
-                for (uint32_t im = mval & rcv_all; im != 0; im &= im - 1u)
+                for (uint32_t im = mv16 & rcv_all; im != 0; im &= im - 1u)
                     place(M(true), (uint32_t)__builtin_ctz(im), bitI, winv);
             }
         }

@@ -444,7 +444,25 @@ def valu_issue(prof, wave_rounds):
             "lds_bank_conflict_frac": (prof["sq_lds_bank_conflict"] / prof["sq_lds_idx_active"]
                                        if prof.get("sq_lds_idx_active") else None),
             "l2_hit_rate": prof.get("l2_hit_rate"),
+            "vector_pipe": vector_pipe(prof, wr),
             "source": f"{prof.get('source')} (committed rocprofv3 --pmc run, not this process)"}
+
+
+def vector_pipe(prof, wave_rounds):
+    """VALU pipe occupancy model: the PMC VALU count split by the static opcode mix of the
+    round loop (tools/isa_table.py --json, committed) into the two measured issue rates of
+    tools/micro/valu_ops (simple ops ~2 SIMD cycles per wave64 instruction, three-operand
+    ops, selects, compares and bit-field ops ~4), against the SIMD cycles available."""
+    path = ROOT / "profiles" / "isa_table.json"
+    if not path.exists() or not prof.get("kernel_ms"):
+        return None
+    isa = json.loads(path.read_text())
+    f = isa["valu_full_fraction"]
+    cyc = prof["valu_per_launch"] / wave_rounds * (2.0 * f + 4.0 * (1.0 - f))
+    avail = prof["kernel_ms"] / 1e3 * 2.4e9 * 1024 / wave_rounds  # 256 CUs x 4 SIMDs at 2.4 GHz
+    return {"cycles_per_wave_round": cyc, "available_per_wave_round": avail, "busy_frac": cyc / avail,
+            "full_rate_fraction": f, "basis": "model: 2 / 4 SIMD cycles per full / half-rate wave64 VALU "
+            "(tools/micro/valu_ops), static mix from profiles/isa_table.json"}
 
 
 def run_kind(dash, args, kind_name, M, sys_base, world, dev, steps, tier_flag):

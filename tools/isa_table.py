@@ -2,7 +2,7 @@
 """Instruction table of the round loop of the headline kernel.
 
 Disassembles the gfx950 code object inside libdash.so, finds the round loop of
-sim_kernel<8, 4, 16, false> (the outermost backward branch of the kernel) and counts its
+sim_kernel<8, 4, 16, false> (the tightest backward branch around four arrival exchanges) and counts its
 instructions by encoding and unit: VOP1/VOP2/VOPC in their 32-bit forms, VOP3 (64-bit
 encodings: three-operand ops, SGPR-mask selects and compares, modifiers), SDWA, SALU, LDS,
 VMEM, branches, waits. Counts are static, over one trip of the loop (DASH_QCHECK = 4
@@ -13,7 +13,7 @@ PMC run (profiles/pmc_uniform.json) for comparison.
 VALU rate classes come from tools/micro/valu_ops.hip (profiles/r01/micro/valu_ops.txt):
 "full" ops issue at 1.4-1.7 wave64 per cycle per CU, "half" ops at 0.94-0.96.
 
-Usage: python3 tools/isa_table.py [libdash.so] [kernel-symbol]
+Usage: python3 tools/isa_table.py [libdash.so] [kernel-symbol] [--json out.json]
 """
 import collections
 import os
@@ -108,12 +108,16 @@ def rate(op):
 
 
 def main():
-    lib = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "ue22cs343bb1-openmp-assignment_amd", "libdash.so")
-    sym = sys.argv[2] if len(sys.argv) > 2 else SYM
+    args = [a for i, a in enumerate(sys.argv[1:], 1) if a != "--json" and sys.argv[i - 1] != "--json"]
+    lib = args[0] if args else os.path.join(ROOT, "ue22cs343bb1-openmp-assignment_amd", "libdash.so")
+    sym = args[1] if len(args) > 1 else SYM
     insns = kernel_insns(extract(lib), sym)
-    # the round loop: the backward branch spanning the most code
+    # the round loop: the tightest backward branch around one trip's ROUNDS_PER_TRIP arrival
+    # exchanges (ds_wrxchg, one per round)
     back = [(x["tgt"], x["off"]) for x in insns if x["tgt"] is not None and x["tgt"] <= x["off"]]
-    lo, hi = max(back, key=lambda b: b[1] - b[0])
+    xchg = [x["off"] for x in insns if x["op"].startswith("ds_wrxchg")]
+    cands = [b for b in back if sum(b[0] <= o <= b[1] for o in xchg) >= ROUNDS_PER_TRIP]
+    lo, hi = min(cands, key=lambda b: b[1] - b[0])
     body = [x for x in insns if lo <= x["off"] <= hi]
     # nested backward branches = the waterfall loops of the rare blocks
     # (other branches back to the loop header are latches of the same loop)
@@ -156,6 +160,15 @@ def main():
     print("\ntop opcodes (per trip):")
     for op, n in ops.most_common(24):
         print(f"  {n:4d}  {op:28s} {unit({'op': op}):22s} {rate(op) if op.startswith('v_') else ''}")
+    if "--json" in sys.argv:
+        import json
+        out = {"kernel": sym, "rounds_per_trip": r, "source": "tools/isa_table.py (static, round loop "
+               "without its waterfall loops)", "per_round": {k: tab[k] / r for k in order if tab[k]},
+               "valu_rate_class_per_round": {k: rates[k] / r for k in ("full", "full*", "half", "half*")},
+               "valu_full_fraction": nf / max(nf + nh, 1),
+               "pipe_model_cycles_per_round": (2 * nf + 4 * nh) / r}
+        with open(sys.argv[sys.argv.index("--json") + 1], "w") as f:
+            json.dump(out, f, indent=1)
     pmc = os.path.join(ROOT, "profiles", "pmc_uniform.json")
     if os.path.exists(pmc):
         import json

@@ -133,7 +133,8 @@ typedef struct dash_gen {
 /* One logged step of one node (cfg.trace_events > 0), in lockstep order. */
 #define DASH_EV_MSG 0u   /* handled a message: word = message word (type[3:0], sender[6:4],
                             address[14:8], value|bitVector[23:16], secondReceiver[26:24];
-                            the other bits are zero) */
+                            the other bits are zero; a REPLY_ID's bitVector is the directory's,
+                            the receiving requester leaves itself out of the INV fan-out) */
 #define DASH_EV_INSTR 1u /* issued an instruction: word = packed instruction */
 typedef struct dash_event {
     uint32_t round;

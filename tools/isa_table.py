@@ -11,7 +11,8 @@ rounds, unrolled) and divided by 4 per round; the rare blocks behind wave-unifor
 PMC run (profiles/pmc_uniform.json) for comparison.
 
 VALU rate classes come from tools/micro/valu_ops.hip (profiles/r01/micro/valu_ops.txt):
-"full" ops issue at 1.4-1.7 wave64 per cycle per CU, "half" ops at 0.94-0.96.
+"full" ops issue at 1.4-1.7 wave64 per cycle per CU, "half" ops at 0.90-0.96 (left shifts,
+selects, compares, bit-field and three-operand ops, SDWA).
 
 Usage: python3 tools/isa_table.py [libdash.so] [kernel-symbol] [--json out.json]
 """
@@ -27,14 +28,19 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 SYM = "_ZN4dash10sim_kernelILi8ELi4ELj16ELb0EEEvNS_7SimArgsE"
 ROUNDS_PER_TRIP = 4
 
-# measured in tools/micro/valu_ops.hip (32 waves/CU): wave64 VALU per cycle per CU
-FULL = {"v_xor_b32": 1.42, "v_and_b32": 1.70, "v_lshrrev_b32": 1.50, "v_sub_u32": 1.48,
-        "v_subrev_u32": 1.48, "v_mov_b32": 1.50}
+# measured in tools/micro/valu_ops.hip (32 waves/CU, profiles/r01/micro/valu_ops.txt and
+# profiles/r02/valu_ops_r2.txt): wave64 VALU per cycle per CU. Left shifts are slow, right
+# shifts fast; bitop3 and the clamped subtract are fast.
+FULL = {"v_xor_b32": 1.42, "v_and_b32": 1.70, "v_lshrrev_b32": 1.50, "v_sub_u32": 1.71,
+        "v_subrev_u32": 1.48, "v_mov_b32": 1.50, "v_add_u32": 1.46, "v_or_b32": 1.51,
+        "v_bitop3_b32": 1.64}
 HALF = {"v_max_u32": 0.96, "v_cndmask_b32": 0.94, "v_cmp_eq_u32": 0.96, "v_bfe_u32": 0.95,
         "v_lshl_or_b32": 0.94, "v_or3_b32": 0.94, "v_bcnt_u32_b32": 0.95, "v_pk_add_u16": 0.94,
-        "v_bfi_b32": 0.94}
+        "v_bfi_b32": 0.94, "v_ffbl_b32": 0.90, "v_perm_b32": 0.94, "v_lshl_add_u32": 0.94,
+        "v_and_or_b32": 0.95, "v_lshlrev_b32": 0.96, "v_add3_u32": 0.93, "v_mad_u32_u24": 0.94,
+        "v_cmp_gt_i32": 0.94}
 # same datapath as a measured op (assumption, marked in the table)
-LIKE_FULL = ("v_or_b32", "v_add_u32", "v_lshlrev_b32", "v_not_b32", "v_ashrrev_i32")
+LIKE_FULL = ("v_not_b32", "v_ashrrev_i32")
 
 
 def extract(lib):
@@ -97,6 +103,8 @@ def unit(x):
 
 
 def rate(op):
+    if op.endswith("_sdwa"):
+        return "half"  # SDWA forms measured slow (shift, compare)
     base = re.sub(r"_(e32|e64|sdwa|dpp)$", "", op)
     if base in FULL:
         return "full"

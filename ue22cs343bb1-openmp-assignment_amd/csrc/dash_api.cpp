@@ -512,8 +512,9 @@ int dash_read_events(dash_t* h, uint64_t sys, dash_event* out, uint32_t cap, uin
             out[k].node = (uint32_t)best;
             out[k].kind = (e[0] & 0x80000000u) ? DASH_EV_INSTR : DASH_EV_MSG;
             // a message word without the kernel's internal bits (7: REPLY_RD's dirState,
-            // 15: the reply-table flag), as include/dash.h documents it
-            out[k].word = (e[0] & 0x80000000u) ? e[1] : e[1] & 0x07FF7F7Fu;
+            // 15: the reply-table flag, 27..24) and with secondReceiver moved from bits 30..28
+            // to 26..24, as include/dash.h documents it
+            out[k].word = (e[0] & 0x80000000u) ? e[1] : (e[1] & 0x00FF7F7Fu) | (((e[1] >> 28) & 7u) << 24);
         }
         ++k;
         ++pos[best];

@@ -62,10 +62,10 @@ using wchunk_t = typename std::conditional<WCHUNK == 4, uint2, uint32_t>::type;
 // message word (ref `message`, :70-79, 20 B -> 4 B):
 //   [3:0] type  [6:4] sender  [7] dirState == S (REPLY_RD)  [14:8] address
 //   [15] the sender's reply-table flag (ignored)  [23:16] value | bitVector
-//   [26:24] secondReceiver  [31:27] zero (secondReceiver is one shift, no field extract)
+//   [27:24] ignored  [30:28] secondReceiver  [31] zero (secondReceiver is one shift)
 __device__ __forceinline__ uint32_t mk(uint32_t type, uint32_t sender, uint32_t addr,
                                        uint32_t val, uint32_t sr, uint32_t ds_s) {
-    return type | (sender << 4) | (ds_s << 7) | (addr << 8) | (val << 16) | (sr << 24);
+    return type | (sender << 4) | (ds_s << 7) | (addr << 8) | (val << 16) | (sr << 28);
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
@@ -112,6 +112,12 @@ __device__ __forceinline__ bool B(mask_t m) { return __builtin_amdgcn_inverse_ba
 __device__ __forceinline__ uint64_t vote(bool c) { return __builtin_amdgcn_ballot_w64(c); }
 // bit 7 / bit 15 of a lane value as a lane mask: one SDWA compare of the sign-extended low
 // byte / half word (the selector would otherwise extract the bit first)
+// 2x as an add (the compiler would turn x + x into a left shift, a slow-kind VALU)
+__device__ __forceinline__ uint32_t dbl(uint32_t x) {
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+}
 // index of the lowest set bit, all ones for 0 (v_ffbl_b32; the callers never use the 0 case)
 __device__ __forceinline__ uint32_t ffbl(uint32_t v) {
     uint32_t r;
@@ -235,8 +241,13 @@ void sim_kernel(const SimArgs a) {
     uint32_t nev = 0;         // events logged (DEBUG_MSG / DEBUG_INSTR emission, off unless a.events)
     // loop-invariant uniform values a round needs, kept in VGPRs: the round's lane masks
     // need the SGPRs (spilling them costs VALU)
-    uint32_t cap = a.max_rounds, nlim = N * 16u, rcv_all = rcv_mask;
+    // rcv_all: the nodes a REPLY_ID fan-out reaches (every node of the system but this one:
+    // the reply carries the directory's whole bitVector, the requester leaves itself out)
+    uint32_t cap = a.max_rounds, nlim = N * 16u, rcv_all = rcv_mask & ~(1u << t);
     asm volatile("" : "+v"(cap), "+v"(nlim), "+v"(rcv_all));
+    // bitop3 masks of the row offsets (bits 10..7 of mw >> 1: block; the cache index's low bits)
+    uint32_t k_ent = 0x780u, k_cac = CS ? ((uint32_t)CS - 1u) << 7 : 0u;
+    asm volatile("" : "+v"(k_ent), "+v"(k_cac));
 
     // eviction notice (ref :767-804), sender part by the line state: EVICT_MODIFIED for M,
     // EVICT_SHARED otherwise; byte k of evb is the first message byte for line state k
@@ -265,18 +276,24 @@ void sim_kernel(const SimArgs a) {
 
     // field source table, same index as the reply table: a v_perm selector that assembles
     // bytes 1..3 of the reply (address, value field, secondReceiver; byte 0 zero). Pool bytes:
-    // 0..3 = mw (0: the issued value, 1: the address, 2: the message value, 3: the message's
-    // secondReceiver), 4 = memory, 5 = the line's value, 6 = sharers less sender, 7 = sender
+    // 0..3 = mw (0: the issued value, or the message's type | sender << 4; 1: the address;
+    // 2: the message value; 3: the message's secondReceiver << 4), 4 = memory, 5 = the
+    // line's value, 6 = the directory's bitVector. secondReceiver sits in bits 30..28, the
+    // high nibble of byte 3, so a byte copy of a message's byte 0 names its sender
     const uint32_t vstab = [&] {
         const uint32_t st = lane >> 2, d = lane & 3;
         uint32_t src = 4u;                                           // memory (RR, ES, ...)
         if (st == T_WBINV || st == T_WBINT) src = 5u;                // written-back line value
-        if (st == T_UPG || (st == T_WRQ && d != D_EM)) src = 6u;     // sharers to invalidate
+        // sharers to invalidate (ref :438-445 sends bitVector less the requester; the requester
+        // leaves itself out when it fans the INVs out, :364-373, which is the same set)
+        if (st == T_UPG || (st == T_WRQ && d != D_EM)) src = 6u;
         if (st == T_WRQ && d == D_EM) src = 2u;                      // forwarded write value
         if (st == 14 || st == 15) src = 0u;                          // issued value
-        // a forwarded request's reply passes its secondReceiver on (ref :281, :498); other
-        // sends name the message's sender (the requester, for a forward)
-        const uint32_t sr = (st == T_WBINV || st == T_WBINT) ? 3u : 7u;
+        // a forwarded request's reply passes its secondReceiver on (ref :281, :498); a forward
+        // (RR / WRQ at EM) names the requester, the message's sender (:219, :441); no other
+        // receiver reads the field
+        const uint32_t sr = (st == T_WBINV || st == T_WBINT) ? 3u
+                            : ((st == T_RR || st == T_WRQ) && d == D_EM) ? 0u : 0x0Cu;
         return 0x0000010Cu | (src << 16) | (sr << 24);  // byte 0: 0x0C selects zero
     }();
     // round counter: rv (a VGPR copy, so the lane masks keep the SGPRs) is the round of
@@ -326,12 +343,27 @@ void sim_kernel(const SimArgs a) {
         const uint32_t mw = B(mHas) ? m : ins;
         uint32_t addr;  // (mw >> 8) & 0x7F as one bfe (the selector would split it into a shift and an and)
         asm("v_bfe_u32 %0, %1, 8, 7" : "=v"(addr) : "v"(mw));
-        const uint32_t b = addr & 15u;
         const uint32_t H = addr >> 4;  // procNodeAddr (ref :186, :657)
-        // cacheIndex = blockIndex % CACHE_SIZE (ref :188)
-        const uint32_t idx = CS ? b % (uint32_t)CS : (uint32_t)(a.cs_lut >> (4 * b)) & 15u;
-        // byte offsets of the row entries; they stay in VGPRs from the loads to the stores
-        uint32_t eoff = (b << 7) | sw2, coff = (idx << 7) | sw2;
+        // byte offsets of the row entries (block << 7 | lane byte; cacheIndex = blockIndex %
+        // CACHE_SIZE, ref :188) and the 2-bit field offsets 2 * block, 2 * cacheIndex, from
+        // right shifts of the word and one bitop3 each: left shifts and shift-ors are
+        // slow-kind VALU (tools/micro/valu_ops)
+        uint32_t eoff, coff, b2, i2;
+        if constexpr (CS != 0) {
+            const uint32_t x1 = mw >> 1, x7 = mw >> 7;
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(eoff) : "v"(x1), "v"(k_ent), "v"(sw2));
+            asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xea" : "=v"(coff) : "v"(x1), "v"(k_cac), "v"(sw2));
+            b2 = x7 & 0x1Eu;
+            i2 = x7 & (2u * ((uint32_t)CS - 1u));
+        } else {
+            const uint32_t b = addr & 15u;
+            const uint32_t idx = (uint32_t)(a.cs_lut >> (4 * b)) & 15u;
+            eoff = (b << 7) | sw2;
+            coff = (idx << 7) | sw2;
+            b2 = dbl(b);
+            i2 = dbl(idx);
+        }
+        // they stay in VGPRs from the loads to the stores
         asm volatile("" : "+v"(eoff), "+v"(coff));
         uint16_t* const ent = reinterpret_cast<uint16_t*>(ldsb + L::ENT * 4 + eoff);
         uint16_t* const cac = reinterpret_cast<uint16_t*>(ldsb + L::CAC * 4 + coff);
@@ -385,12 +417,12 @@ void sim_kernel(const SimArgs a) {
         const uint32_t sty = B(mDo) ? (ins >> 15) | 14u : pty;  // step type: 14 / 15 = issue RD / WR
         const mask_t miR = M(sty == 14u), miW = M(sty == 15u);
 
-        const uint32_t bv = e16 >> 8, ds = (dsv >> (2 * b)) & 3u;
-        const uint32_t laddr = c16 & 0xFFu, lst = (cst >> (2 * idx)) & 3u;
+        const uint32_t bv = e16 >> 8, ds = (dsv >> b2) & 3u;
+        const uint32_t laddr = c16 & 0xFFu, lst = (cst >> i2) & 3u;
         // the message's value field in bits 7..0 (secondReceiver above it: every consumer
         // takes the low byte only -- a byte permute, a u16 store, an AND)
         const uint32_t msender = (m >> 4) & 7u, mv16 = mw >> 16;
-        const uint32_t msr = m >> 24;  // bits 31..27 are zero
+        const uint32_t msr = m >> 28;  // bit 31 is zero
         const uint32_t sbit = 1u << msender;
 
         const mask_t mEM = M(ds == D_EM), mS = M(ds == D_S), mU = ~(mEM | mS);
@@ -457,7 +489,7 @@ void sim_kernel(const SimArgs a) {
         // REPLY_RD carries dirState == S in bit 27 (the other receivers ignore it)
         tA = B(miW & mHit) ? (uint32_t)T_UPG : tA;
         const uint32_t vsel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((sty << 4) | (ds << 2)), (int)vstab);
-        const uint32_t vpool = __builtin_amdgcn_perm(c16, e16, 0x0C0C0500u) | (es_bv << 16) | (msender << 24);
+        const uint32_t vpool = __builtin_amdgcn_perm(c16, e16, 0x0C010500u);  // [mem, lval, bv, 0]
         const uint32_t av16 = __builtin_amdgcn_perm(vpool, mw, vsel);  // address and value fields, in place
         const uint32_t wA = tA | (t << 4) | av16;  // bit 15 of the address byte: ignored
         const uint32_t dE = laddr >> 4;
@@ -485,8 +517,9 @@ void sim_kernel(const SimArgs a) {
         uint32_t cw = B(mFill) ? (addr | (fval << 8)) : c16;
         asm volatile("" : "+v"(cw));
         *cac = (uint16_t)cw;
-        dsv = (dsv & ~(3u << (2 * b))) | (nds << (2 * b));
-        cst = (cst & ~(3u << (2 * idx))) | (nst << (2 * idx));
+        // field updates as xor-of-differences: three plain VALU ops each (no bitop3)
+        dsv ^= (ds ^ nds) << b2;
+        cst ^= (lst ^ nst) << i2;
 
         // ---- end-of-round delivery: lowest sender first, program order within a sender ----
         // Each node publishes its queue tail and count (after this round's pop);

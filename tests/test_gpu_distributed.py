@@ -68,3 +68,22 @@ def test_bench_spawns_two_ranks_without_torchrun():
     assert d2["totals"] == d1["totals"]
     assert d2["contention"]["totals"] == d1["contention"]["totals"]
     assert d2["contention"]["totals"]["instructions_per_step"] == 4096 * 8 * 512
+
+
+def test_rccl_collectives_one_rank():
+    """The RCCL path itself (backend nccl: init_process_group with the device, barriers and the
+    MAX / SUM all-reduces of reduce_totals) on the box's one GPU, as a one-rank group: the
+    totals equal a run without a process group (the 8-GPU node runs this code per rank)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK",
+                                                            "MASTER_ADDR", "MASTER_PORT")}
+    pg = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--process-group", "--dist-backend", "nccl",
+                         "--contention-steps", "1"] + ARGS,
+                        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert pg.returncode == 0, pg.stderr[-3000:]
+    dp = _line(pg.stdout)
+    one = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--contention-steps", "1"] + ARGS,
+                         capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = _line(one.stdout)
+    assert dp["n_gpus"] == 1
+    assert dp["totals"] == d1["totals"] and dp["contention"]["totals"] == d1["contention"]["totals"]

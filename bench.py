@@ -449,6 +449,13 @@ def valu_issue(prof, wave_rounds):
                                        if prof.get("sq_lds_idx_active") else None),
             "l2_hit_rate": prof.get("l2_hit_rate"),
             "vector_pipe": vector_pipe(prof, wr),
+            # measured (SQ_ACTIVE_INST_VALU2, SQ_CYCLES): SIMD quad-cycles that issued one or two
+            # VALU / two VALU, and the mean active lanes of a VALU instruction
+            "issue_slots": ({"busy_frac": prof["valu_issue_busy_frac"], "dual_frac": prof["valu_dual_issue_frac"],
+                             "exec_lanes": prof.get("valu_exec_lanes"),
+                             "basis": "(SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / SIMD quad-cycles; a SIMD "
+                                      "issues at most two VALU per quad-cycle"}
+                            if "valu_issue_busy_frac" in prof else None),
             "source": f"{prof.get('source')} (committed rocprofv3 --pmc run, not this process)"}
 
 

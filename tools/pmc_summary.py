@@ -48,5 +48,16 @@ if "TCC_HIT_sum" in agg and "TCC_MISS_sum" in agg:
 if "SQ_INSTS_VALU" in agg:
     res["valu_per_launch"] = agg["SQ_INSTS_VALU"]
     res["kernel_ms"] = dur["SQ_INSTS_VALU"]
+# VALU issue slots, measured (sq3 pass): SQ_CYCLES is summed over the 32 shader engines
+# (8 XCDs x 4), so SIMD quad-cycles = SQ_CYCLES / 32 x 1024 SIMDs / 4. A SIMD issues at most
+# two VALU per quad-cycle (SQ_ACTIVE_INST_VALU2 counts the quad-cycles that issued two), so
+# quad-cycles with any VALU issue = INSTS_VALU - VALU2
+if "SQ_ACTIVE_INST_VALU2" in agg and "SQ_CYCLES" in agg and "SQ_INSTS_VALU" in agg:
+    q = agg["SQ_CYCLES"] / 32 * 1024 / 4
+    res["simd_quad_cycles"] = q
+    res["valu_issue_busy_frac"] = (agg["SQ_INSTS_VALU"] - agg["SQ_ACTIVE_INST_VALU2"]) / q
+    res["valu_dual_issue_frac"] = agg["SQ_ACTIVE_INST_VALU2"] / q
+if "SQ_THREAD_CYCLES_VALU" in agg and "SQ_INSTS_VALU" in agg:
+    res["valu_exec_lanes"] = agg["SQ_THREAD_CYCLES_VALU"] / agg["SQ_INSTS_VALU"]  # of 64
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

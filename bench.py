@@ -553,6 +553,11 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="BASELINE configs[4]: CACHE_SIZE {1,2,4,8,16} x locality {0,.25,.5,.75,1}, "
                          "systems sharded over the ranks, histograms all-reduced per configuration")
+    ap.add_argument("--next", action="store_true",
+                    help="the SURVEY.md 8(f) rows beside the hot path, measured with a parity property each "
+                         "(bench_next.py): text ingest, digests / dumps, DEBUG event log, seeded schedules")
+    ap.add_argument("--next-systems", type=int, default=2048, help="--next: trace directories written and ingested")
+    ap.add_argument("--next-dir", default=None, help="--next: where the trace directories go (default: $TMPDIR)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="no GPU: the rank launch plus one gloo all-reduce of the shard table on the CPU "
                          "(tests/test_distributed.py checks the launcher with it)")
@@ -606,6 +611,11 @@ def main():
 
     if args.sweep:
         return sweep(args, dash, rank, world, dev)
+    if args.next:
+        if world != 1:
+            raise SystemExit("bench.py --next runs on one GPU")
+        import bench_next
+        return bench_next.run(dash, dev, args)
     if args.host_traces:
         return host_traces(args, dash, rank, world, dev)
 

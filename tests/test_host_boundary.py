@@ -109,3 +109,20 @@ def test_resolve_dir(dash, tmp_path, monkeypatch):
     assert dash.lib().dash_resolve_dir(b"t1", buf, 256) == 0 and buf.value == b"tests/t1"
     assert dash.lib().dash_resolve_dir(b"tests/t1", buf, 256) == 0 and buf.value == b"tests/t1"
     assert dash.lib().dash_resolve_dir(b"nope", buf, 256) == dash.EIO
+
+
+def test_bench_next_trace_text_round_trips(dash, tmp_path):
+    """bench.py --next writes its ingest workload as core_<n>.txt text (bench_next.trace_text);
+    the library's parser (the reference's fgets + sscanf rules) must read back the same words,
+    RD values as 0 (ref :839)."""
+    import sys
+    sys.path.insert(0, str(pathlib.Path(__file__).resolve().parent.parent))
+    import bench_next
+    rng = np.random.default_rng(11)
+    w = rng.bit_generator.random_raw(1024).view(np.uint16).copy()
+    w[:3] = [0x8000, 0x80FF, 0x7F00 | 0x55]  # WR 0x00 0, WR 0x00 255, RD 0x7F (value dropped)
+    f = tmp_path / "core_0.txt"
+    f.write_bytes(bench_next.trace_text(w))
+    assert f.read_text().splitlines()[:3] == ["WR 0x00 0", "WR 0x00 255", "RD 0x7F"]
+    got = dash.parse_core_file(f, num_procs=8, max_instr=len(w))
+    assert np.array_equal(got, np.where(w & 0x8000, w, w & 0xFF00).astype(np.uint16))

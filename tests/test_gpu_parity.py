@@ -331,6 +331,16 @@ def test_seeded_schedule_bit_exact(dash, seed, N, CS):
     check_batch(dash, packed, lens, N, CS, seed=seed)
 
 
+def test_seeded_schedule_past_the_round_table(dash, monkeypatch):
+    """The seeded schedule's per-round words come from a table built at dash_create; rounds past
+    its end hash their key in the kernel. With the table cut to 8 rounds (DASH_ARB_TABLE, read at
+    dash_create) most rounds take that path: still bit-exact vs the oracle's twin."""
+    monkeypatch.setenv("DASH_ARB_TABLE", "8")
+    rng = np.random.default_rng(44)
+    packed, lens = random_batch(rng, 64, 8, 48, hot_frac=0.3)
+    check_batch(dash, packed, lens, 8, 4, seed=0xABCDEF)
+
+
 def test_seeded_schedule_reaches_other_accepted_run(dash, tmp_path):
     """test_4 accepts run_1..run_4 (test4.sh); lockstep gives run_1, the seeded
     schedule 87 gives run_2 -- both legal serialisations."""

@@ -39,6 +39,8 @@ struct dash_ctx {
     uint32_t* d_list[2] = {nullptr, nullptr};  // overflow hand-off lists (ping-pong)
     uint32_t* d_count = nullptr;
     uint32_t* d_events = nullptr;       // [(sys*N+node)*trace_events][2]
+    uint32_t* d_arb = nullptr;          // seeded schedule: one word per round (dash::arb_word)
+    uint32_t arb_len = 0;
     uint32_t* d_event_count = nullptr;  // [sys*N+node]
     uint64_t tier_systems[dash::NUM_TIERS] = {};  // systems run per queue-depth tier, last run
     int auto_tier = 0;                         // adaptive first tier
@@ -116,6 +118,7 @@ static void release(dash_t* h) {
     (void)hipFree(h->d_event_count);
     (void)hipFree(h->d_hint);
     (void)hipFree(h->d_skip);
+    (void)hipFree(h->d_arb);
     if (h->side) (void)hipStreamSynchronize(h->side);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     if (h->ev_join) (void)hipEventDestroy(h->ev_join);
@@ -199,6 +202,16 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     if (cfg->trace_events) {
         chk(hipMalloc(&h->d_events, std::max<uint64_t>(nsys * N * cfg->trace_events, 1) * 8), "hipMalloc(events)");
         chk(hipMalloc(&h->d_event_count, std::max<uint64_t>(nsys * N, 1) * 4), "hipMalloc(event_count)");
+    }
+    if (cfg->schedule_seed) {  // the seeded schedule's round words, built once per handle
+        // DASH_ARB_TABLE (tests only) shortens the table so the in-kernel hashing past its end runs
+        const char* e = getenv("DASH_ARB_TABLE");
+        const uint64_t cap = e ? (strtoull(e, nullptr, 0) & ~3ull) : dash::ARB_TABLE_MAX;
+        h->arb_len = (uint32_t)std::min<uint64_t>(h->cfg.max_rounds, std::min<uint64_t>(cap, dash::ARB_TABLE_MAX));
+        chk(hipMalloc(&h->d_arb, ((uint64_t)h->arb_len + 4) * sizeof(uint32_t)), "hipMalloc(arb)");
+        if (rc == DASH_OK) chk(dash::launch_arb_table(cfg->schedule_seed, h->seg, h->d_arb, h->arb_len, h->stream),
+                               "arb table");
+        if (rc == DASH_OK) chk(hipStreamSynchronize(h->stream), "arb table");
     }
     if (cfg->flags & DASH_KEEP_STATE)
         chk(hipMalloc(&h->d_state, std::max<uint64_t>(nsys * N, 1) * (16 + CS) * sizeof(uint32_t)),
@@ -311,6 +324,8 @@ int dash_run(dash_t* h, dash_stats* stats) {
     a.keep = (h->cfg.flags & DASH_KEEP_STATE) ? 1u : 0u;
     a.event_cap = h->cfg.trace_events;
     a.arb_seed = h->cfg.schedule_seed;
+    a.arb_tab = h->d_arb;
+    a.arb_len = h->arb_len;
     a.cache_size = h->cfg.cache_size;
     for (uint32_t b = 0; b < 16; b++)  // b % CACHE_SIZE for the generic (non-power-of-two) kernels
         a.cs_lut |= (uint64_t)(b % h->cfg.cache_size) << (4 * b);

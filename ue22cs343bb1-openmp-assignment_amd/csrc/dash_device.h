@@ -51,6 +51,8 @@ struct SimArgs {
     uint32_t* event_count;    // [sys*N+node] events produced (may exceed event_cap)
     unsigned long long* stats;  // [STAT_WORDS]
     uint64_t arb_seed;        // 0: lowest-sender-first lockstep; else the seeded schedule
+    const uint32_t* arb_tab;  // seeded schedule: per-round word (arb_word) for rounds < arb_len
+    uint32_t arb_len;         // a multiple of 4; rounds beyond it hash their key in the kernel
     const uint8_t* skip;      // optional [sys]: 1 = run elsewhere this pass (a deeper tier, concurrently)
     uint32_t cache_size;      // CACHE_SIZE (ref :7); read by the generic (non-power-of-two) kernels
     uint64_t cs_lut;          // nibble b = b % cache_size, b < 16 (generic kernels)
@@ -83,6 +85,9 @@ constexpr uint32_t CHUNK_INSTR = 4;  // instructions per 8-B trace chunk
 // its last instruction (never issued), so the last lane's stream needs no bounds test
 constexpr uint64_t TRACE_PAD = 64;
 hipError_t launch_gen(const GenArgs& g, hipStream_t s);
+// the seeded schedule's per-round words (arb_word) for rounds [0, n), n a multiple of 4
+constexpr uint32_t ARB_TABLE_MAX = 1u << 24;
+hipError_t launch_arb_table(uint64_t seed, uint32_t seg, uint32_t* out, uint32_t n, hipStream_t s);
 // skip[list[i]] = 1 for i < n
 // RD words carry value 0 (ref :839): clears bits 7..0 of every word whose bit 15 is 0
 hipError_t launch_clear_rd(uint2* trace, uint64_t words, hipStream_t s);

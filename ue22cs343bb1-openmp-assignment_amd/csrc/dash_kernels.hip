@@ -77,6 +77,20 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
     return k;
 }
 
+// The seeded schedule's round: its key is fmix64(seed ^ round * golden), a node
+// t < P sits the round out when bits 8t+1..8t of fmix64(key' ^ const) are zero, and senders
+// deliver in the affine order (t * A + Bc) & (P - 1) with A = (key & (P - 1)) | 1 and
+// Bc = (key >> 8) & (P - 1). One word per round: bit t = node t stalls, A in bits 10..8, Bc in
+// bits 13..11. The oracle twins (orc_arb_stall / orc_arb_prio) compute the same.
+__device__ __forceinline__ uint32_t arb_word(uint64_t seed, uint32_t round, uint32_t P) {
+    const uint64_t rk = seed ^ ((uint64_t)round * 0x9E3779B97F4A7C15ull);
+    const uint64_t key = fmix64(rk), skey = fmix64(rk ^ 0xD1B54A32D192ED03ull);
+    uint32_t w = 0;
+    for (uint32_t t = 0; t < P; ++t) w |= (((skey >> (8 * t)) & 3u) == 0 ? 1u : 0u) << t;
+    const uint32_t A = ((uint32_t)key & (P - 1)) | 1u, Bc = (uint32_t)(key >> 8) & (P - 1);
+    return w | (A << 8) | (Bc << 11);
+}
+
 // CS = CACHE_SIZE; CS = 0 is the generic kernel for a non-power-of-two CACHE_SIZE (read at
 // run time, LDS sized for the maximum of 16 lines)
 template <int CS>
@@ -300,6 +314,9 @@ void sim_kernel(const SimArgs a) {
     // the trip's first step; the step at position k of the trip is round rv + k
     uint32_t rv = 0;
     asm volatile("" : "+v"(rv));
+    // seeded schedule: this trip's four round words, and the next trip's (in flight)
+    uint4 arbw = make_uint4(0, 0, 0, 0), arbn = make_uint4(0, 0, 0, 0);
+    if (SLOW && a.arb_seed && a.arb_len) arbn = *reinterpret_cast<const uint4*>(a.arb_tab);
 #if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU) || defined(DASH_PAD_VHALF)
     uint32_t padv[4] = {lane, lane + 1, lane + 2, lane + 3}, pads[4] = {0, 1, 2, 3};
 #endif
@@ -322,11 +339,16 @@ void sim_kernel(const SimArgs a) {
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
         mask_t mStall = 0;
         uint32_t bitI = 1u << (4 * t);
-        if (SLOW && a.arb_seed) {  // round keys are wave-uniform: computed on the scalar unit
-            const uint64_t rk = a.arb_seed ^ ((uint64_t)__builtin_amdgcn_readfirstlane(rv + k) * 0x9E3779B97F4A7C15ull);
-            const uint64_t key = fmix64(rk), skey = fmix64(rk ^ 0xD1B54A32D192ED03ull);
-            mStall = M(((skey >> (8 * t)) & 3u) == 0);
-            const uint32_t A = ((uint32_t)key & (P - 1)) | 1u, Bc = (uint32_t)(key >> 8) & (P - 1);
+        if (SLOW && a.arb_seed) {
+            // the round's word from the table (loaded a trip ahead), or hashed past its end;
+            // either way wave-uniform
+            uint32_t w = k == 0 ? arbw.x : k == 1 ? arbw.y : k == 2 ? arbw.z : arbw.w;
+            if (rv + k >= a.arb_len) {
+                COLD();
+                w = arb_word(a.arb_seed, __builtin_amdgcn_readfirstlane(rv + k), P);
+            }
+            mStall = M(((w >> t) & 1u) != 0);
+            const uint32_t A = (w >> 8) & 7u, Bc = (w >> 11) & 7u;
             bitI = 1u << (4 * ((t * A + Bc) & (P - 1)));
         }
         const mask_t mHas = mMsg & ~mStall;           // pops this round
@@ -656,6 +678,10 @@ void sim_kernel(const SimArgs a) {
             }
         }
         refill();
+        if (SLOW && a.arb_seed) {
+            arbw = arbn;
+            if (rv + 4 < a.arb_len) arbn = *reinterpret_cast<const uint4*>(a.arb_tab + rv + 4);
+        }
         step(0, mMsg, mIss);
 #pragma unroll
         for (uint32_t k = 1; k < WCHUNK; ++k) step(k, can_pop(), can_issue());
@@ -872,6 +898,18 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring
     default: return hipErrorInvalidValue;
     }
 #endif
+}
+
+__global__ __launch_bounds__(256) void arb_table_kernel(uint64_t seed, uint32_t P, uint32_t* out, uint32_t n) {
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
+        out[r] = arb_word(seed, r, P);
+}
+
+hipError_t launch_arb_table(uint64_t seed, uint32_t seg, uint32_t* out, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(arb_table_kernel, dim3(blocks), dim3(256), 0, s, seed, seg, out, n);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void clear_rd_kernel(uint2* trace, uint64_t words) {

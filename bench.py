@@ -24,8 +24,11 @@ Prints ONE JSON line on rank 0 (contract in the task statement).
 
 Other modes (not the headline): --kind contention (configs[3]); --sweep (configs[4]);
 --host-traces [--host-batches B] [--host-native]: traces handed over from host memory every
-step (PCIe-inclusive rate of the drop-in boundary); --cpu-kind reference:
-the reference binary itself as the CPU baseline.
+step (PCIe-inclusive rate of the drop-in boundary); --next: the SURVEY §8(f)
+rows beside the hot path (text ingest, digests / dumps, DEBUG event log, seeded schedules),
+each with a parity property (bench_next.py); --process-group: run the collectives as a
+one-rank group (the RCCL path on a 1-GPU box); --cpu-kind port: the oracle restatement as
+the CPU baseline instead of the reference binary.
 """
 import argparse
 import json

@@ -3,9 +3,10 @@
 tests/golden/full_size.json holds the oracle's totals over ALL 2^20 systems of BASELINE
 configs[2] (uniform) and [3] (contention), made by tests/golden/make_full_size.py. The
 bench lines committed under profiles/r01/ were measured on an MI355X over exactly those
-workloads; their per-type histograms, round totals and error-system counts must equal the
-oracle's (bit-exact), so every committed headline number is a run with the reference's
-results. The live GPU check of the same fixture is
+workloads, and so is the round-2 headline line profiles/r02/bench_headline.json (its
+uniform totals and its `contention` object); their per-type histograms, round totals and
+error-system counts must equal the oracle's (bit-exact), and the round-2 line's digest
+checksum too, so every committed headline number is a run with the reference's results. The live GPU check of the same fixture is
 test_gpu_parity.py::test_full_size_sampled_parity (adds the digest checksum).
 """
 import json
@@ -36,3 +37,17 @@ def test_committed_gpu_bench_matches_oracle(kind):
     assert tot["instructions_per_step"] == g["instructions"]
     assert tot["rounds_total"] == g["rounds_total"]
     assert tot["err_systems"] == g["err_systems"]
+
+
+@pytest.mark.parametrize("kind", list(BENCH))
+def test_round2_headline_line_matches_oracle(kind):
+    line = json.loads((ROOT / "profiles" / "r02" / "bench_headline.json").read_text())
+    assert line["config"]["systems_per_gpu"] == GOLD["systems"] and line["n_gpus"] == 1
+    assert line["config"]["trace"] == "uniform" and line["config"]["cache_size"] == GOLD["cache_size"]
+    tot = line["totals"] if kind == "uniform" else line["contention"]["totals"]
+    g = GOLD[kind]
+    assert tot["hist"] == g["hist"]
+    assert tot["instructions_per_step"] == g["instructions"]
+    assert tot["rounds_total"] == g["rounds_total"]
+    assert tot["err_systems"] == g["err_systems"]
+    assert tot["digest_sum"] == g["digest_sum"]

@@ -280,6 +280,20 @@ def test_cli_debug_flags(dash, tmp_path):
             (GOLDEN / "sample" / f"core_{n}_output.txt").read_bytes()
 
 
+def test_cli_schedule_seed(dash, tmp_path):
+    """`cache_simulator test_4 --schedule 87`: the drop-in CLI with a seeded legal schedule lands
+    on the accepted run_2 (test4.sh); without the option it gives run_1 (lockstep)."""
+    exe = dash.PKG / "cache_simulator"
+    (tmp_path / "tests").mkdir()
+    shutil.copytree(GOLDEN / "test_4", tmp_path / "tests" / "test_4")
+    for args, run in (([], "run_1"), (["--schedule", "87"], "run_2")):
+        p = subprocess.run([str(exe), "test_4"] + args, cwd=tmp_path, capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        for n in range(4):
+            assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
+                (GOLDEN / "test_4" / run / f"core_{n}_output.txt").read_bytes(), (run, n)
+
+
 def test_bulk_dirs_ingest_and_dump(dash, tmp_path):
     """Trace-directory ingest at scale (ref :822-850 per directory) and bulk
     printProcessorState emission: 40 directories in one batch."""

@@ -12,6 +12,8 @@
  *   --debug-instr / --debug-msg  print the reference's DEBUG_INSTR (:650-651) /
  *       DEBUG_MSG (:180-181) lines to stdout, in lockstep order (the reference's
  *       -D DEBUG_INSTR / -D DEBUG_MSG builds, README :104)
+ *   --schedule SEED   a seeded legal schedule instead of lowest-sender-first (DESIGN.md §2;
+ *       e.g. --schedule 87 lands tests/test_4 on its accepted run_2); also in bulk modes
  *
  * Bulk modes (one GPU batch, many systems; dumps go to OUT_DIR/<k>/):
  *   --batch LIST        system k = the k-th trace directory listed in LIST (one per line)
@@ -31,9 +33,9 @@ static const char *txn_names[DASH_NUM_TXN] = {
     "READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID", "INV", "UPGRADE",
     "WRITEBACK_INV", "WRITEBACK_INT", "FLUSH", "FLUSH_INVACK", "EVICT_SHARED", "EVICT_MODIFIED"};
 
-/* dash_simulate_dir plus the event log of the one system */
+/* dash_simulate_dir plus a schedule seed and the event log of the one system */
 static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m, const char *out, int dev,
-                           int dbg_instr, int dbg_msg, dash_stats *st) {
+                           int dbg_instr, int dbg_msg, unsigned long long sched, dash_stats *st) {
     dash_cfg cfg = {0};
     cfg.num_procs = n;
     cfg.cache_size = cs;
@@ -41,7 +43,8 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
     cfg.flags = DASH_KEEP_STATE;
     cfg.num_systems = 1;
     cfg.device = dev;
-    cfg.trace_events = 1u << 16;
+    cfg.trace_events = (dbg_instr || dbg_msg) ? 1u << 16 : 0;
+    cfg.schedule_seed = sched;
     dash_t *h = NULL;
     int rc = dash_create(&cfg, &h);
     if (rc != DASH_OK) return rc;
@@ -54,7 +57,7 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
             rc = dash_dump_file(&nodes[t], t, cs, path);
         }
         uint32_t cap = cfg.trace_events * n, total = 0;
-        dash_event *ev = (dash_event *)malloc(sizeof(dash_event) * cap);
+        dash_event *ev = cap ? (dash_event *)malloc(sizeof(dash_event) * cap) : NULL;
         if (rc == DASH_OK && ev) {
             int erc = dash_read_events(h, 0, ev, cap, &total);
             for (uint32_t k = 0; k < total && k < cap; k++) {
@@ -73,7 +76,7 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
 
 typedef struct {
     unsigned n, cs, m, len, kind, locality;
-    unsigned long long seed;
+    unsigned long long seed, sched;
     int dev, show;
     const char *out, *digests, *dump;
 } bulk_opts;
@@ -125,6 +128,7 @@ static int run_batch_list(const char *list, const bulk_opts *o) {
     cfg.flags = DASH_KEEP_STATE;
     cfg.num_systems = n;
     cfg.device = o->dev;
+    cfg.schedule_seed = o->sched;
     dash_t *h = NULL;
     dash_stats st;
     int rc = n ? dash_create(&cfg, &h) : DASH_EINVAL;
@@ -147,6 +151,7 @@ static int run_synthetic(uint64_t count, const bulk_opts *o) {
     cfg.flags = o->dump ? DASH_KEEP_STATE : 0;
     cfg.num_systems = count;
     cfg.device = o->dev;
+    cfg.schedule_seed = o->sched;
     dash_gen g = {0};
     g.seed = o->seed;
     g.kind = o->kind;
@@ -170,7 +175,7 @@ int main(int argc, char *argv[]) {
     unsigned n = 4, cs = 4, m = 32;
     int dev = 0, show = 0, dbg_instr = 0, dbg_msg = 0, n_given = 0;
     const char *out = ".", *dir = NULL, *batch = NULL, *digests = NULL, *dump = NULL;
-    unsigned long long synth = 0, seed = 0x5EED;
+    unsigned long long synth = 0, seed = 0x5EED, sched = 0;
     unsigned len = 4096, kind = DASH_GEN_UNIFORM;
     double loc = 0.5;
     for (int i = 1; i < argc; i++) {
@@ -188,6 +193,7 @@ int main(int argc, char *argv[]) {
         else if (!strcmp(argv[i], "--dump") && i + 1 < argc) dump = argv[++i];
         else if (!strcmp(argv[i], "--len") && i + 1 < argc) len = (unsigned)atoi(argv[++i]);
         else if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = strtoull(argv[++i], NULL, 0);
+        else if (!strcmp(argv[i], "--schedule") && i + 1 < argc) sched = strtoull(argv[++i], NULL, 0);
         else if (!strcmp(argv[i], "--locality") && i + 1 < argc) loc = atof(argv[++i]);
         else if (!strcmp(argv[i], "--kind") && i + 1 < argc) {
             const char *k = argv[++i];
@@ -198,7 +204,7 @@ int main(int argc, char *argv[]) {
     }
     if (batch || synth) {
         if (synth && !n_given) n = 8; /* synthetic systems default to 8 nodes (BASELINE configs) */
-        bulk_opts o = {n, cs, m, len, kind, (unsigned)(loc * 65536.0), seed, dev, show, out, digests, dump};
+        bulk_opts o = {n, cs, m, len, kind, (unsigned)(loc * 65536.0), seed, sched, dev, show, out, digests, dump};
         if (o.locality > 65536u) o.locality = 65536u;
         int rc = batch ? run_batch_list(batch, &o) : run_synthetic(synth, &o);
         return rc == DASH_OK ? EXIT_SUCCESS : EXIT_FAILURE;
@@ -208,8 +214,8 @@ int main(int argc, char *argv[]) {
         return EXIT_FAILURE;
     }
     dash_stats st;
-    int rc = (dbg_instr || dbg_msg) ? simulate_traced(dir, n, cs, m, out, dev, dbg_instr, dbg_msg, &st)
-                                    : dash_simulate_dir(dir, n, cs, m, out, dev, &st);
+    int rc = (dbg_instr || dbg_msg || sched) ? simulate_traced(dir, n, cs, m, out, dev, dbg_instr, dbg_msg, sched, &st)
+                                             : dash_simulate_dir(dir, n, cs, m, out, dev, &st);
     if (rc != DASH_OK) {
         const char *why = dash_last_error(NULL);
         fprintf(stderr, "cache_simulator: %s (%d)\n", why[0] ? why : "failed", rc);

@@ -561,6 +561,8 @@ def main():
                          "(bench_next.py): text ingest, digests / dumps, DEBUG event log, seeded schedules")
     ap.add_argument("--next-systems", type=int, default=2048, help="--next: trace directories written and ingested")
     ap.add_argument("--next-dir", default=None, help="--next: where the trace directories go (default: $TMPDIR)")
+    ap.add_argument("--next-event-systems", type=int, default=32768,
+                    help="--next: systems of the DEBUG event-log row (device-generated traces)")
     ap.add_argument("--dist-selftest", action="store_true",
                     help="no GPU: the rank launch plus one gloo all-reduce of the shard table on the CPU "
                          "(tests/test_distributed.py checks the launcher with it)")

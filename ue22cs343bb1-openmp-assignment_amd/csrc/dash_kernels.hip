@@ -80,15 +80,16 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
 // The seeded schedule's round: its key is fmix64(seed ^ round * golden), a node
 // t < P sits the round out when bits 8t+1..8t of fmix64(key' ^ const) are zero, and senders
 // deliver in the affine order (t * A + Bc) & (P - 1) with A = (key & (P - 1)) | 1 and
-// Bc = (key >> 8) & (P - 1). One word per round: bit t = node t stalls, A in bits 10..8, Bc in
-// bits 13..11. The oracle twins (orc_arb_stall / orc_arb_prio) compute the same.
+// Bc = (key >> 8) & (P - 1). One word per round: bit t = node t stalls, bits 8 + 3t .. 10 + 3t =
+// node t's delivery position. The oracle twins (orc_arb_stall / orc_arb_prio) compute the same.
 __device__ __forceinline__ uint32_t arb_word(uint64_t seed, uint32_t round, uint32_t P) {
     const uint64_t rk = seed ^ ((uint64_t)round * 0x9E3779B97F4A7C15ull);
     const uint64_t key = fmix64(rk), skey = fmix64(rk ^ 0xD1B54A32D192ED03ull);
-    uint32_t w = 0;
-    for (uint32_t t = 0; t < P; ++t) w |= (((skey >> (8 * t)) & 3u) == 0 ? 1u : 0u) << t;
     const uint32_t A = ((uint32_t)key & (P - 1)) | 1u, Bc = (uint32_t)(key >> 8) & (P - 1);
-    return w | (A << 8) | (Bc << 11);
+    uint32_t w = 0;
+    for (uint32_t t = 0; t < P; ++t)
+        w |= ((((skey >> (8 * t)) & 3u) == 0 ? 1u : 0u) << t) | (((t * A + Bc) & (P - 1)) << (8 + 3 * t));
+    return w;
 }
 
 // CS = CACHE_SIZE; CS = 0 is the generic kernel for a non-power-of-two CACHE_SIZE (read at
@@ -340,16 +341,11 @@ void sim_kernel(const SimArgs a) {
         mask_t mStall = 0;
         uint32_t bitI = 1u << (4 * t);
         if (SLOW && a.arb_seed) {
-            // the round's word from the table (loaded a trip ahead), or hashed past its end;
-            // either way wave-uniform
-            uint32_t w = k == 0 ? arbw.x : k == 1 ? arbw.y : k == 2 ? arbw.z : arbw.w;
-            if (rv + k >= a.arb_len) {
-                COLD();
-                w = arb_word(a.arb_seed, __builtin_amdgcn_readfirstlane(rv + k), P);
-            }
+            // the round's word (wave-uniform): from the table, loaded a trip ahead, or hashed at
+            // the trip start past the table's end
+            const uint32_t w = k == 0 ? arbw.x : k == 1 ? arbw.y : k == 2 ? arbw.z : arbw.w;
             mStall = M(((w >> t) & 1u) != 0);
-            const uint32_t A = (w >> 8) & 7u, Bc = (w >> 11) & 7u;
-            bitI = 1u << (4 * ((t * A + Bc) & (P - 1)));
+            bitI = 1u << (((w >> (8 + 3 * t)) & 7u) << 2);
         }
         const mask_t mHas = mMsg & ~mStall;           // pops this round
         const mask_t mDo = mIss & ~mMsg & ~mStall;    // issues this round
@@ -655,6 +651,7 @@ void sim_kernel(const SimArgs a) {
     // test and the trace window refill
     constexpr uint32_t TRIP = DASH_QCHECK;
     static_assert(TRIP == WCHUNK || TRIP == 2 * WCHUNK, "one or two refill blocks per trip");
+    static_assert(!SLOW || TRIP == 4, "the seeded schedule reads four round words per trip");
     mask_t mMsg = can_pop(), mIss = can_issue();
     // quiescence is absorbing, so testing it once per trip only adds idle rounds (no
     // state changes, not counted in `rounds`)
@@ -681,6 +678,12 @@ void sim_kernel(const SimArgs a) {
         if (SLOW && a.arb_seed) {
             arbw = arbn;
             if (rv + 4 < a.arb_len) arbn = *reinterpret_cast<const uint4*>(a.arb_tab + rv + 4);
+            if (rv >= a.arb_len) {  // past the table (arb_len is a multiple of 4, like rv)
+                COLD();
+                const uint32_t r0 = __builtin_amdgcn_readfirstlane(rv);
+                arbw = make_uint4(arb_word(a.arb_seed, r0, P), arb_word(a.arb_seed, r0 + 1, P),
+                                  arb_word(a.arb_seed, r0 + 2, P), arb_word(a.arb_seed, r0 + 3, P));
+            }
         }
         step(0, mMsg, mIss);
 #pragma unroll

@@ -96,34 +96,47 @@ def cpu_baseline(args, seed, kind, locality, target_s):
     res = oc.run_batch(seed, 0, count, num_procs=8, cache_size=args.cache_size, length=args.len,
                        kind=kind, locality=locality, threads=threads)
     return {"value": res["instructions"] / res["seconds"], "unit": "instr/s", "cores": threads,
-            "kind": "port", "cpu_model": cpu_model(),
+            "host_cpus_visible": host_cpus_visible(), "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{count} systems x 8 nodes x {args.len} instr ({args.kind}, CS={args.cache_size}, "
                       f"seed 0x{seed:X}) in {res['seconds']:.1f} s on {threads} threads; "
                       f"oracle/dash_oracle.c lockstep restatement of assignment.c"}
 
 
-def ref_baseline(args, seed, kind_id, target_s):
-    """The reference itself (oracle/_ref/cache_simulator_bench: assignment.c with the
+def host_cpus_visible():
+    """Logical CPUs the machine exposes (the quota in host_cores() is what a job may use)."""
+    return os.cpu_count() or 1
+
+
+def ref_exe(cache_size):
+    """oracle/_ref/cache_simulator_bench (CACHE_SIZE 4) or ..._cs<C> (oracle/patch_ref.py)."""
+    name = "cache_simulator_bench" + ("" if cache_size == 4 else f"_cs{cache_size}")
+    return ROOT / "oracle" / "_ref" / name
+
+
+def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, locality=0, kind_name=None):
+    """The reference itself (oracle/_ref/cache_simulator_bench[_cs<C>]: assignment.c with the
     benchmark patch of SURVEY.md §8(d), gcc -O2 -fopenmp, 8 spinning OpenMP threads per
     instance) on systems 0.. of the same synthetic workload, written as the reference's
-    tests/<dir>/core_<n>.txt. `--ref-instances` processes run concurrently (the north
-    star's "as many concurrent instances as host cores"; 1 = one 8-thread instance);
-    batches repeat until `target_s` has passed."""
+    tests/<dir>/core_<n>.txt. `instances` processes run concurrently (0 = one per host core,
+    BASELINE.md mode (A): the north star's "as many concurrent instances as host cores";
+    1 = mode (B), one 8-thread instance); batches repeat until `target_s` has passed (at
+    least one batch)."""
     import subprocess
     import tempfile
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_ctypes as oc
-    exe = ROOT / "oracle" / "_ref" / "cache_simulator_bench"
+    exe = ref_exe(cache_size)
     if not exe.exists():
         raise RuntimeError(f"{exe.relative_to(ROOT)} missing (built by __graft_entry__.build() / "
                            f"oracle/build_ref.sh where /root/reference exists)")
-    k = args.ref_instances or host_cores()
+    k = instances or host_cores()
+    kind_name = kind_name or args.kind
     with tempfile.TemporaryDirectory() as td:
         dirs = []
         for i in range(k):
             d = pathlib.Path(td, f"i{i}")
             (d / "tests" / "b").mkdir(parents=True)
-            tr = oc.gen_system(seed, i, num_procs=8, length=args.len, kind=kind_id)
+            tr = oc.gen_system(seed, i, num_procs=8, length=args.len, kind=kind_id, locality=locality)
             for n in range(8):
                 lines = []
                 for w in tr[n].tolist():
@@ -158,13 +171,15 @@ def ref_baseline(args, seed, kind_id, target_s):
             assert all((d / f"core_{n}_output.txt").exists() for n in range(8)), d
     instr = batches * k * 8 * args.len
     cores = host_cores()
-    return {"value": instr / elapsed, "unit": "instr/s", "cores": cores, "kind": "reference",
-            "mode": "A" if k == cores else ("B" if k == 1 else f"{k} instances"),
-            "cpu_model": cpu_model(),
+    loc = f", locality {locality / 65536:g}" if kind_name == "locality" else ""
+    return {"value": instr / elapsed, "unit": "instr/s", "cores": cores, "host_cpus_visible": host_cpus_visible(),
+            "kind": "reference", "mode": "A" if k == cores else ("B" if k == 1 else f"{k} instances"),
+            "instances": k, "threads_per_instance": 8, "cpu_model": cpu_model(),
             "sample": f"{batches} batch(es) x {k} concurrent instance(s) x 8 OpenMP threads, one 8-node system "
-                      f"x {args.len} instr each ({args.kind}, CS=4, systems 0..{k - 1} of seed 0x{seed:X}) "
-                      f"in {elapsed:.1f} s on {cores} host cores ({cpu_model()}); assignment.c + benchmark "
-                      f"patch (oracle/patch_ref.py), gcc -O2 -fopenmp"}
+                      f"x {args.len} instr each ({kind_name}{loc}, CS={cache_size}, systems 0..{k - 1} of seed "
+                      f"0x{seed:X}) in {elapsed:.1f} s; {cores} CPUs of cgroup quota on a host exposing "
+                      f"{host_cpus_visible()} logical CPUs ({cpu_model()}); assignment.c + benchmark patch "
+                      f"(oracle/patch_ref.py), gcc -O2 -fopenmp"}
 
 
 def shard(rank, world, per_gpu):
@@ -194,36 +209,34 @@ def digest_sum(digests):
     return [int((d & np.uint64(0xFFFFFFFF)).sum(dtype=np.uint64)), int((d >> np.uint64(32)).sum(dtype=np.uint64))]
 
 
-def read_profile(kind):
+def kernel_fingerprint(lib_path):
+    """sha256 prefix of the headline kernel's code + descriptor in the library being run
+    (tools/kernel_fingerprint.py), or None if it cannot be read."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    try:
+        import kernel_fingerprint as kf
+        return kf.fingerprint(lib_path)
+    except Exception:
+        return None
+
+
+def read_profile(kind, fp):
     """Per-launch counters of the first-tier sim_kernel from the committed rocprofv3
-    PMC summary for this workload (tools/pmc_summary.py), or None."""
+    PMC summary for this workload (tools/pmc_summary.py), only if it was measured on the
+    code object being run: (profile or None, note). `fp` = kernel_fingerprint of the
+    library this process loaded."""
     f = ROOT / "profiles" / f"pmc_{kind}.json"
-    if f.exists():
-        try:
-            return json.loads(f.read_text())
-        except Exception:
-            return None
-    return None
-
-
-def timed_runs(eng, args, world, dev):
-    import torch
-    import torch.distributed as dist
-
-    def barrier():
-        if dist.is_initialized():
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        eng.run()
-    barrier()
-    t0 = time.perf_counter()
-    stats = None
-    for _ in range(args.steps):
-        stats = eng.run()
-    barrier()
-    return time.perf_counter() - t0, stats
+    if not f.exists():
+        return None, f"{f.relative_to(ROOT)} missing"
+    try:
+        prof = json.loads(f.read_text())
+    except Exception as e:
+        return None, f"{f.relative_to(ROOT)} unreadable: {e}"
+    if fp is None or prof.get("kernel_fingerprint") != fp:
+        return None, (f"{f.relative_to(ROOT)} was measured on kernel {prof.get('kernel_fingerprint')}, this run's "
+                      f"sim_kernel<8,4,16,false> is {fp}: its counters do not describe this binary, so traffic "
+                      f"and issue figures are omitted")
+    return prof, None
 
 
 def sweep(args, dash, rank, world, dev):
@@ -236,34 +249,54 @@ def sweep(args, dash, rank, world, dev):
     points = []
     for cs in (1, 2, 4, 8, 16):
         for p in (0.0, 0.25, 0.5, 0.75, 1.0):
+            loc = int(round(p * 65536))
             eng = dash.Engine(M, num_procs=8, cache_size=cs, max_instr=args.len, device=dev)
-            eng.generate(args.seed, args.len, kind=dash.GEN_LOCALITY, locality=int(round(p * 65536)),
-                         sys_base=sys_base)
-            elapsed, stats = timed_runs(eng, args, world, dev)
+            eng.generate(args.seed, args.len, kind=dash.GEN_LOCALITY, locality=loc, sys_base=sys_base)
+            elapsed, stats, kms = timed_headline(eng, args, world, dev)
             dsum = digest_sum(eng.read_results()[0])
             elapsed, totals = reduce_totals(
                 elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
                                           stats["dropped"]] + dsum, torch.device("cuda", dev), world)
             eng.close()
+            avg_s = sum(kms) / len(kms) / 1e3
             points.append({"cache_size": cs, "locality": p,
                            "value": world * M * 8 * args.len * args.steps / elapsed,
                            "ms_per_step": elapsed / args.steps * 1e3,
-                           "kernel_ms": stats["kernel_ms"],
+                           # this rank's first-tier launches over the timed steps (HIP events; the step
+                           # time above is the max over ranks of the whole timed region)
+                           "kernel_ms_avg": avg_s * 1e3, "kernel_ms_steps": [round(x, 3) for x in kms],
+                           "roofline": roofline(M, args.len, avg_s, None,
+                                                "no committed PMC run for sweep points: traffic not measured"),
                            "rounds_per_system": totals[14] / (world * M),
                            "hist": totals[:13], "instructions": totals[13], "rounds_total": totals[14],
                            "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19],
                            "tier_systems": stats["tier_systems"]})
+    if dist.is_initialized():
+        dist.destroy_process_group()
     if rank == 0:
+        # the reference itself per point (mode (A), one batch or more of --sweep-cpu-seconds), after
+        # every GPU point and after the process group is gone (any --gpus N)
+        for pt in points:
+            pt["cpu_baseline"], pt["vs_baseline"], pt["cpu_baseline_note"] = None, None, None
+            if args.no_cpu_baseline:
+                continue
+            try:
+                cpu = ref_baseline(args, args.seed, dash.GEN_LOCALITY, args.sweep_cpu_seconds, args.ref_instances,
+                                   cache_size=pt["cache_size"], locality=int(round(pt["locality"] * 65536)),
+                                   kind_name="locality")
+                pt["cpu_baseline"], pt["vs_baseline"] = cpu, pt["value"] / cpu["value"]
+            except Exception as e:  # reported, never substituted by the port
+                pt["cpu_baseline_note"] = f"reference baseline unavailable: {e}"
         print(json.dumps({"metric": "simulated instr/sec (whole node), 8-core DASH systems; sweep",
                           "unit": "instr/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "higher_is_better": True, "scaling": "weak", "dtype": "u8",
                           "data": "synthetic locality traces (on-device generator, seed keyed by global id)",
                           "config": {"workload": f"{world * M} systems ({M}/GPU) x 8 nodes x {args.len} "
-                                                 f"instr, CACHE_SIZE x locality grid",
+                                                 f"instr, CACHE_SIZE x locality grid (BASELINE configs[4])",
                                      "parallelism": f"systems sharded over {world} GPU(s)"},
+                          "vs_baseline_basis": "per point: value / cpu_baseline.value (the reference binary built "
+                                               "for that CACHE_SIZE, mode (A), on systems 0.. of that point's traces)",
                           "sweep": points}), flush=True)
-    if dist.is_initialized():
-        dist.destroy_process_group()
 
 
 def host_trace_batch(seed, M, L):
@@ -424,16 +457,18 @@ def timed_headline(eng, args, world, dev):
     return time.perf_counter() - t0, stats, kernel_ms
 
 
-def roofline(M, args, avg_kernel_s, prof):
+def roofline(M, length, avg_kernel_s, prof, note=None):
     """Algorithmic bytes per launch (2 B per simulated instruction) over the
     launch's average duration (HIP events on the engine's stream), against 8 TB/s;
     `traffic` = HBM bytes per launch of the same kernel from the committed rocprofv3 PMC
-    run (profiles/pmc_<kind>.json, tools/pmc_summary.py), not from this process."""
-    achieved = M * 8 * args.len * BYTES_PER_INSTR / avg_kernel_s
+    run (profiles/pmc_<kind>.json, tools/pmc_summary.py), not from this process, and only
+    when that run's kernel fingerprint is this binary's (else null, `traffic_note` says why)."""
+    achieved = M * 8 * length * BYTES_PER_INSTR / avg_kernel_s
     return {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
             "frac": achieved / PEAK_HBM, "traffic": prof.get("hbm_bytes_per_launch") if prof else None,
             "traffic_source": (f"{prof.get('source')} (committed rocprofv3 --pmc run of this kernel, "
-                               f"per launch)") if prof else None}
+                               f"per launch; kernel fingerprint {prof.get('kernel_fingerprint')})") if prof else None,
+            "traffic_note": note}
 
 
 def valu_issue(prof, wave_rounds):
@@ -471,6 +506,8 @@ def vector_pipe(prof, wave_rounds):
     if not path.exists() or not prof.get("kernel_ms"):
         return None
     isa = json.loads(path.read_text())
+    if isa.get("kernel_fingerprint") != prof.get("kernel_fingerprint"):
+        return None  # static mix of another code object
     f = isa["valu_full_fraction"]
     cyc = prof["valu_per_launch"] / wave_rounds * (2.0 * f + 4.0 * (1.0 - f))
     avail = prof["kernel_ms"] / 1e3 * 2.4e9 * 1024 / wave_rounds  # 256 CUs x 4 SIMDs at 2.4 GHz
@@ -525,7 +562,10 @@ def main():
                     help="timed steps of the contention workload (configs[3]) reported in the headline "
                          "line's `contention` object (0 = skip); its own warmup step precedes them")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target seconds of each CPU leg (reference mode A, mode B, oracle port)")
+    ap.add_argument("--sweep-cpu-seconds", type=float, default=1.0,
+                    help="--sweep: target seconds of the reference baseline per point (at least one batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-kind", choices=["port", "reference"], default="reference",
                     help="headline cpu_baseline: the reference binary itself (oracle/_ref/cache_simulator_bench, "
@@ -632,14 +672,15 @@ def main():
     value = instr_per_step * args.steps / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     full = M == 1 << 20 and args.len == 4096 and args.cache_size == 4
-    prof = read_profile(args.kind) if full else None
+    fp = kernel_fingerprint(dash.LIB_PATH)
+    prof, prof_note = read_profile(args.kind, fp) if full else (None, "committed PMC runs are of the full-size workload")
 
     # configs[3] beside the headline: its own warmup and timed steps (same barriers)
     cont = None
     if args.contention_steps > 0 and args.kind == "uniform":
         c_el, c_tot, c_stats, c_kms = run_kind(dash, args, "contention", M, sys_base, world, dev,
                                                args.contention_steps, tier_flag)
-        c_prof = read_profile("contention") if full else None
+        c_prof, c_note = read_profile("contention", fp) if full else (None, prof_note)
         c_avg = sum(c_kms) / len(c_kms) / 1e3
         cont = {"workload": f"{M} systems/GPU x 8 nodes x {args.len} contention RD/WR per node (90 % WR to "
                             f"0x00-0x03), CACHE_SIZE={args.cache_size} (BASELINE configs[3])",
@@ -647,25 +688,29 @@ def main():
                 "steps": args.contention_steps, "warmup": args.warmup,
                 "ms_per_step": c_el / args.contention_steps * 1e3,
                 "kernel_ms_avg": c_avg * 1e3, "kernel_ms_steps": [round(x, 3) for x in c_kms],
-                "roofline": roofline(M, args, c_avg, c_prof),
+                "roofline": roofline(M, args.len, c_avg, c_prof, c_note),
                 "valu_issue": valu_issue(c_prof, c_stats["wave_rounds"]),
                 "tier_systems": c_stats["tier_systems"], "wave_rounds": c_stats["wave_rounds"],
                 "totals": totals_dict(c_tot)}
 
+    # the CPU legs run after the timed regions and after the process group is gone, on rank 0
+    # only, for every --gpus N (the ratio north_star states is the 8-GPU one)
+    if dist.is_initialized():
+        dist.destroy_process_group()
     if rank == 0:
-        cpu, port, note = None, None, None
-        if world == 1 and not args.no_cpu_baseline:
+        cpu, cpu_b, port, note = None, None, None, None
+        if not args.no_cpu_baseline:
             kind_id = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
                        "locality": dash.GEN_LOCALITY}[args.kind]
             locality = int(round(args.locality * 65536)) if args.kind == "locality" else 0
             if args.cpu_kind == "reference":
-                if args.cache_size != 4 or args.kind == "locality":
-                    note = "the reference baseline binary is built for CACHE_SIZE 4, uniform/contention traces"
-                else:
-                    try:
-                        cpu = ref_baseline(args, args.seed, kind_id, args.cpu_seconds)
-                    except Exception as e:  # reported, never substituted by the port
-                        note = f"reference baseline unavailable: {e}"
+                try:  # BASELINE.md mode (A): one instance per host core; mode (B): one instance
+                    cpu = ref_baseline(args, args.seed, kind_id, args.cpu_seconds, args.ref_instances,
+                                       args.cache_size, locality)
+                    if not args.ref_instances:
+                        cpu_b = ref_baseline(args, args.seed, kind_id, args.cpu_seconds, 1, args.cache_size, locality)
+                except Exception as e:  # reported, never substituted by the port
+                    note = f"reference baseline unavailable: {e}"
             port = cpu_baseline(args, args.seed, kind_id, locality, args.cpu_seconds)
             if args.cpu_kind == "port":
                 cpu, port = port, None
@@ -685,6 +730,7 @@ def main():
                                   + (f", mode {cpu['mode']}" if cpu.get("mode") else "")
                                   + ", measured on this box's host in this run; BASELINE.md publishes no number)")
             if cpu else None,
+            "vs_baseline_mode_b": value / cpu_b["value"] if cpu_b else None,
             "dtype": "u8",
             "data": "synthetic (on-device counter-based generator, seed keyed by global system id)",
             "config": {"workload": f"{M} systems/GPU x 8 nodes x {args.len} {args.kind} RD/WR per node, "
@@ -692,10 +738,13 @@ def main():
                        "systems_per_gpu": M, "num_procs": 8, "instr_per_node": args.len,
                        "cache_size": args.cache_size, "trace": args.kind,
                        "parallelism": f"systems sharded over {world} GPU(s)"},
-            "roofline": roofline(M, args, avg_kernel_s, prof),
+            "roofline": roofline(M, args.len, avg_kernel_s, prof, prof_note),
             # what binds this integer state machine: instruction issue
             "valu_issue": valu_issue(prof, stats["wave_rounds"]),
+            "valu_issue_note": prof_note,
+            "kernel_fingerprint": fp,
             "cpu_baseline": cpu,
+            "cpu_baseline_mode_b": cpu_b,
             "cpu_baseline_note": note,
             "cpu_port": port,
             "kernel_ms_avg": avg_kernel_s * 1e3,
@@ -712,8 +761,6 @@ def main():
             "contention": cont,
         }
         print(json.dumps(line), flush=True)
-    if dist.is_initialized():
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -75,6 +75,8 @@ enum dash_txn {
 #define DASH_TIER_FROM_32 2u  /* start at queue depth 32 (testing: exercises that kernel) */
 #define DASH_TIER_FROM_256 4u /* run every system at depth 256 directly; with no TIER flag
                                  the first depth adapts to the previous run's overflow rate */
+#define DASH_TEST_SHORT_ARB 8u /* testing only: the seeded schedule's round table holds 8 rounds,
+                                  so later rounds take the in-kernel hashing path */
 
 typedef struct dash_cfg {
     uint32_t num_procs;   /* NUM_PROCS (ref :6): 4 or 8 */
@@ -83,7 +85,8 @@ typedef struct dash_cfg {
     uint32_t flags;       /* DASH_KEEP_STATE */
     uint64_t num_systems; /* independent systems in the batch */
     uint64_t max_rounds;  /* per-system round cap (engine-defined: the reference never exits),
-                             rounded up to a multiple of 4; 0 = 1024 + 256*max_instr */
+                             clamped to 2^31 - 4, then rounded up to a multiple of 4;
+                             0 = 1024 + 256*max_instr */
     int32_t device;       /* HIP device ordinal */
     uint32_t trace_events; /* per-node event log capacity for DEBUG_MSG / DEBUG_INSTR
                               emission (ref :179-182, :649-652); 0 = no log */

@@ -38,6 +38,13 @@ enum {
     WRITEBACK_INV, WRITEBACK_INT, FLUSH, FLUSH_INVACK, EVICT_SHARED, EVICT_MODIFIED
 };
 
+/* Mutation testing of the reference pin (tests/test_reference_cross_node.py): ORC_MUTANT = k
+   builds oracle/_mut/libdash_oracle_m<k>.so with one plausible misreading of a cross-node
+   handler (listed in tests/ref_pin.py MUTANTS). The shipped checker is ORC_MUTANT 0. */
+#ifndef ORC_MUTANT
+#define ORC_MUTANT 0
+#endif
+
 #define MAX_RING 256
 #define MAX_OUT (ORC_MAX_PROCS + 4)
 
@@ -171,7 +178,8 @@ static void handle_message(osys *sy, int tid, omsg msg) {
         send_message(nd, procNodeAddr, r);
         if (procNodeAddr != msg.secondReceiver)
             send_message(nd, msg.secondReceiver, r);
-        L->state = SHARED;
+        if (ORC_MUTANT != 1 || L->address == msg.address)
+            L->state = SHARED;
         break;
 
     case FLUSH: /* ref :288-323 */
@@ -187,7 +195,8 @@ static void handle_message(osys *sy, int tid, omsg msg) {
             L->value = msg.value;
             L->state = SHARED;
         }
-        nd->waiting = 0; /* unconditional (App. B 2) */
+        if (ORC_MUTANT != 2 || tid == msg.secondReceiver)
+            nd->waiting = 0; /* unconditional (App. B 2) */
         break;
 
     case UPGRADE: { /* ref :325-349; no directory-state check */
@@ -195,7 +204,7 @@ static void handle_message(osys *sy, int tid, omsg msg) {
         r.type = REPLY_ID;
         r.sender = (uint8_t)tid;
         r.address = msg.address;
-        r.bitVector = others;
+        r.bitVector = ORC_MUTANT == 3 ? nd->bitVector[memBlockAddr] : others;
         send_message(nd, msg.sender, r);
         nd->dirState[memBlockAddr] = EM;
         nd->bitVector[memBlockAddr] = (uint8_t)(1u << msg.sender);
@@ -269,7 +278,8 @@ static void handle_message(osys *sy, int tid, omsg msg) {
         r.value = L->value;
         r.secondReceiver = msg.secondReceiver;
         send_message(nd, procNodeAddr, r);
-        send_message(nd, msg.secondReceiver, r);
+        if (ORC_MUTANT != 4 || procNodeAddr != msg.secondReceiver)
+            send_message(nd, msg.secondReceiver, r);
         L->state = INVALID;
         break;
 
@@ -282,7 +292,7 @@ static void handle_message(osys *sy, int tid, omsg msg) {
             if (L->address != msg.address && L->state != INVALID)
                 handle_cache_replacement(nd, tid, *L);
             L->address = msg.address;
-            L->value = nd->instr_value;
+            L->value = ORC_MUTANT == 5 ? msg.value : nd->instr_value;
             L->state = MODIFIED;
         }
         nd->waiting = 0;
@@ -290,7 +300,8 @@ static void handle_message(osys *sy, int tid, omsg msg) {
 
     case EVICT_SHARED: /* ref :538-590 */
         if (tid != procNodeAddr) {
-            L->state = EXCLUSIVE; /* no address check (App. B 5) */
+            if (ORC_MUTANT != 7 || L->address == msg.address)
+                L->state = EXCLUSIVE; /* no address check (App. B 5) */
         } else {
             nd->bitVector[memBlockAddr] &= (uint8_t)~(1u << msg.sender);
             int numSharers = __builtin_popcount(nd->bitVector[memBlockAddr]);
@@ -305,7 +316,7 @@ static void handle_message(osys *sy, int tid, omsg msg) {
                     r.address = msg.address;
                     r.value = nd->memory[memBlockAddr];
                     send_message(nd, newOwner, r);
-                } else {
+                } else if (ORC_MUTANT != 6) {
                     L->state = EXCLUSIVE;
                 }
             }
@@ -425,6 +436,12 @@ uint64_t orc_digest_node(const orc_node_state *s, int node_id, int cache_size) {
     return h;
 }
 
+/* the engine's round cap: clamped to 2^31 - 4 first, then rounded up to a multiple of 4
+   (dash_create does the same) */
+static uint64_t round_cap(uint64_t max_rounds) {
+    return ((max_rounds < 0x7FFFFFFCULL ? max_rounds : 0x7FFFFFFCULL) + 3) & ~3ULL;
+}
+
 int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
                    const uint32_t *lens, orc_result *out, char *log, uint64_t log_cap) {
     const int N = cfg->num_procs, CS = cfg->cache_size;
@@ -463,7 +480,7 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
         }
         if (!active) break;
         /* the engine's round cap (not the reference's: it never exits) is a multiple of 4 */
-        if (cfg->max_rounds && out->rounds >= ((cfg->max_rounds + 3) & ~3ULL)) {
+        if (cfg->max_rounds && out->rounds >= round_cap(cfg->max_rounds)) {
             out->errors |= ORC_ERR_ROUNDCAP;
             break;
         }

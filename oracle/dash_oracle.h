@@ -38,8 +38,13 @@ extern "C" {
 typedef struct orc_cfg {
     int num_procs;       /* N (NUM_PROCS, ref :6) 1..8 */
     int cache_size;      /* CACHE_SIZE (ref :7), 1..16 */
-    int ring_depth;      /* queue capacity: 32 = GPU engine, 256 = ref MSG_BUFFER_SIZE (:9) */
-    uint64_t max_rounds; /* 0 = unlimited; rounded up to a multiple of 4 like the engine's */
+    int ring_depth;      /* queue capacity (ref MSG_BUFFER_SIZE, :9): 256 is the reference and the
+                            engine; a queue that reaches it is stuck (ref :167-170). Smaller
+                            values model a reference built with a smaller MSG_BUFFER_SIZE, NOT
+                            the engine's shallow tiers (the engine re-runs a system that would
+                            exceed a tier at the next depth, so it never freezes below 256) */
+    uint64_t max_rounds; /* 0 = unlimited; else clamped to 2^31 - 4 and rounded up to a
+                            multiple of 4 like the engine's */
     int log_msgs;        /* log also DEBUG_MSG lines (ref :180-181), not only DEBUG_INSTR */
     int _pad;
     uint64_t arb_seed;   /* 0: deliver in ascending sender order; else the seeded per-round

@@ -65,9 +65,21 @@ EDITS = [
 ]
 
 
+# (output name, -D flags). The bench binaries: 8 nodes, 4096 instructions, one per CACHE_SIZE of
+# BASELINE configs[4] (bench.py's cpu_baseline; CACHE_SIZE 4 keeps the round-2 name). The pin
+# binaries: the reference's own 4 nodes / 32 instructions with its DEBUG_MSG trace of every handled
+# message (ref :179-182), for tests/test_reference_cross_node.py (the oracle's cross-node handlers
+# checked against the reference itself).
+TARGETS = [("cache_simulator_bench", ["-DNUM_PROCS=8", "-DMAX_INSTR_NUM=4096", "-DCACHE_SIZE=4"])]
+TARGETS += [(f"cache_simulator_bench_cs{cs}", ["-DNUM_PROCS=8", "-DMAX_INSTR_NUM=4096", f"-DCACHE_SIZE={cs}"])
+            for cs in (1, 2, 8, 16)]
+TARGETS += [(f"cache_simulator_pin_cs{cs}", ["-DNUM_PROCS=4", "-DMAX_INSTR_NUM=32", f"-DCACHE_SIZE={cs}",
+                                              "-DDEBUG_MSG"]) for cs in (1, 4)]
+
+
 def main():
     ref = pathlib.Path(sys.argv[1] if len(sys.argv) > 1 else "/root/reference") / "assignment.c"
-    out = pathlib.Path(__file__).resolve().parent / "_ref" / "cache_simulator_bench"
+    outdir = pathlib.Path(__file__).resolve().parent / "_ref"
     if not ref.exists():
         print(f"reference not present at {ref}; skipping", file=sys.stderr)
         return 0
@@ -77,13 +89,14 @@ def main():
         if n != 1:
             raise SystemExit(f"patch anchor found {n} times: {old[:60]!r}")
         src = src.replace(old, new)
-    out.parent.mkdir(parents=True, exist_ok=True)
+    outdir.mkdir(parents=True, exist_ok=True)
     with tempfile.TemporaryDirectory() as td:
         c = pathlib.Path(td) / "assignment_bench.c"
         c.write_text(src)
-        subprocess.run(["gcc", "-O2", "-fopenmp", "-w", "-DNUM_PROCS=8", "-DMAX_INSTR_NUM=4096",
-                        "-DCACHE_SIZE=4", "-o", str(out), str(c)], check=True)
-    print(f"built {out}")
+        for name, defs in TARGETS:
+            out = outdir / name
+            subprocess.run(["gcc", "-O2", "-fopenmp", "-w"] + defs + ["-o", str(out), str(c)], check=True)
+            print(f"built {out}")
     return 0
 
 

@@ -58,36 +58,41 @@ class OrcGen(ctypes.Structure):
 _lib = None
 
 
+def bind(path):
+    """ctypes binding of an oracle build (the checker, or a mutant of oracle/_mut/)."""
+    L = ctypes.CDLL(str(path))
+    L.orc_run_system.argtypes = [ctypes.POINTER(OrcCfg), ctypes.c_void_p, ctypes.c_uint64,
+                                 ctypes.c_void_p, ctypes.POINTER(OrcResult),
+                                 ctypes.c_char_p, ctypes.c_uint64]
+    L.orc_run_system.restype = ctypes.c_int
+    L.orc_gen_instr.argtypes = [ctypes.POINTER(OrcGen), ctypes.c_uint64, ctypes.c_uint32,
+                                ctypes.c_uint32]
+    L.orc_gen_instr.restype = ctypes.c_uint16
+    L.orc_gen_system.argtypes = [ctypes.POINTER(OrcGen), ctypes.c_uint64, ctypes.c_void_p,
+                                 ctypes.c_uint64]
+    L.orc_run_batch.argtypes = [ctypes.POINTER(OrcCfg), ctypes.POINTER(OrcGen),
+                                ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_void_p]
+    L.orc_run_batch.restype = ctypes.c_double
+    L.orc_dump_node.argtypes = [ctypes.POINTER(OrcNodeState), ctypes.c_int, ctypes.c_int,
+                                ctypes.c_char_p, ctypes.c_int]
+    L.orc_dump_node.restype = ctypes.c_int
+    V, U64 = ctypes.c_void_p, ctypes.c_uint64
+    L.orc_replay_lockstep.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, V]
+    L.orc_random_schedule.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, U64, V]
+    L.orc_explore.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, U64, V, ctypes.c_int, V, V, V]
+    for f in (L.orc_replay_lockstep, L.orc_random_schedule, L.orc_explore):
+        f.restype = ctypes.c_int
+    return L
+
+
 def lib():
     global _lib
     if _lib is None:
         if not ORACLE_SO.exists():
             subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
-        L = ctypes.CDLL(str(ORACLE_SO))
-        L.orc_run_system.argtypes = [ctypes.POINTER(OrcCfg), ctypes.c_void_p, ctypes.c_uint64,
-                                     ctypes.c_void_p, ctypes.POINTER(OrcResult),
-                                     ctypes.c_char_p, ctypes.c_uint64]
-        L.orc_run_system.restype = ctypes.c_int
-        L.orc_gen_instr.argtypes = [ctypes.POINTER(OrcGen), ctypes.c_uint64, ctypes.c_uint32,
-                                    ctypes.c_uint32]
-        L.orc_gen_instr.restype = ctypes.c_uint16
-        L.orc_gen_system.argtypes = [ctypes.POINTER(OrcGen), ctypes.c_uint64, ctypes.c_void_p,
-                                     ctypes.c_uint64]
-        L.orc_run_batch.argtypes = [ctypes.POINTER(OrcCfg), ctypes.POINTER(OrcGen),
-                                    ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
-                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                    ctypes.c_void_p, ctypes.c_void_p]
-        L.orc_run_batch.restype = ctypes.c_double
-        L.orc_dump_node.argtypes = [ctypes.POINTER(OrcNodeState), ctypes.c_int, ctypes.c_int,
-                                    ctypes.c_char_p, ctypes.c_int]
-        L.orc_dump_node.restype = ctypes.c_int
-        V, U64 = ctypes.c_void_p, ctypes.c_uint64
-        L.orc_replay_lockstep.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, V]
-        L.orc_random_schedule.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, U64, V]
-        L.orc_explore.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, U64, V, ctypes.c_int, V, V, V]
-        for f in (L.orc_replay_lockstep, L.orc_random_schedule, L.orc_explore):
-            f.restype = ctypes.c_int
-        _lib = L
+        _lib = bind(ORACLE_SO)
     return _lib
 
 
@@ -184,16 +189,18 @@ def random_schedule(trace, lens, seed, num_procs=4, cache_size=4):
     return out
 
 
-def explore(trace, lens, num_procs=4, cache_size=4, max_states=1_000_000, max_outs=4096):
+def explore(trace, lens, num_procs=4, cache_size=4, max_states=1_000_000, max_outs=4096, L=None):
     """Exhaustive search of the race-free micro-step model (pop-first persistent
-    sets). Returns (distinct outcomes, states visited, complete)."""
+    sets). Returns (distinct outcomes, states visited, complete). `L`: another oracle
+    build (bind()), e.g. a mutant."""
     trace, lens = _tr(trace, lens)
+    L = L or lib()
     cfg = OrcCfg(num_procs, cache_size, 256, 0)
     outs = (OrcOutcome * max_outs)()
     n = ctypes.c_int()
     states = ctypes.c_uint64()
     full = ctypes.c_int()
-    rc = lib().orc_explore(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1], lens.ctypes.data,
+    rc = L.orc_explore(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1], lens.ctypes.data,
                            max_states, ctypes.addressof(outs), max_outs, ctypes.addressof(n),
                            ctypes.addressof(states), ctypes.addressof(full))
     if rc != 0:
@@ -201,9 +208,9 @@ def explore(trace, lens, num_procs=4, cache_size=4, max_states=1_000_000, max_ou
     return [outs[k] for k in range(min(n.value, max_outs))], int(states.value), bool(full.value)
 
 
-def dump_node(res, node, cache_size=4) -> str:
+def dump_node(res, node, cache_size=4, L=None) -> str:
     buf = ctypes.create_string_buffer(8192)
-    n = lib().orc_dump_node(ctypes.byref(res.node[node]), node, cache_size, buf, 8192)
+    n = (L or lib()).orc_dump_node(ctypes.byref(res.node[node]), node, cache_size, buf, 8192)
     return buf.raw[:n].decode()
 
 

@@ -70,6 +70,26 @@ def test_bench_spawns_two_ranks_without_torchrun():
     assert d2["contention"]["totals"]["instructions_per_step"] == 4096 * 8 * 512
 
 
+def test_multi_gpu_line_carries_the_reference_baseline():
+    """the --gpus N line (the one north_star's 8-GPU target is read from)
+    carries the reference baseline in both BASELINE.md modes and the ratio to it. Two ranks
+    here (gloo, the one GPU); the CPU legs run on rank 0 after the process group is gone."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--contention-steps", "0", "--cpu-seconds", "0.5"] + ARGS[:-1],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2
+    a, b = d["cpu_baseline"], d["cpu_baseline_mode_b"]
+    assert a["kind"] == b["kind"] == "reference", d["cpu_baseline_note"]
+    assert a["mode"] == "A" and a["instances"] == a["cores"] and b["mode"] == "B" and b["instances"] == 1
+    assert a["host_cpus_visible"] >= a["cores"]
+    assert abs(d["vs_baseline"] - d["value"] / a["value"]) < 1e-9 * d["vs_baseline"]
+    assert abs(d["vs_baseline_mode_b"] - d["value"] / b["value"]) < 1e-9 * d["vs_baseline_mode_b"]
+    assert d["cpu_port"]["kind"] == "port"
+
+
 def test_rccl_collectives_one_rank():
     """The RCCL path itself (backend nccl: init_process_group with the device, barriers and the
     MAX / SUM all-reduces of reduce_totals) on the box's one GPU, as a one-rank group: the

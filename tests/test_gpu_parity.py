@@ -205,6 +205,8 @@ def test_round_cap(dash):
     packed, lens = random_batch(rng, 40, 4, 32, fixed_len=True)
     check_batch(dash, packed, lens, 4, 4, max_rounds=20)
     check_batch(dash, packed, lens, 4, 4, max_rounds=21)  # rounded up to 24 by both
+    # clamped to 2^31 - 4 before rounding up ((2^64 - 1 + 3) & ~3 used to wrap to 0)
+    check_batch(dash, packed[:8], lens[:8], 4, 4, max_rounds=(1 << 64) - 1)
 
 
 @pytest.mark.parametrize("kind,loc", [(0, 0), (1, 0), (2, 49152), (2, 0), (2, 65536)])
@@ -345,14 +347,13 @@ def test_seeded_schedule_bit_exact(dash, seed, N, CS):
     check_batch(dash, packed, lens, N, CS, seed=seed)
 
 
-def test_seeded_schedule_past_the_round_table(dash, monkeypatch):
+def test_seeded_schedule_past_the_round_table(dash):
     """The seeded schedule's per-round words come from a table built at dash_create; rounds past
-    its end hash their key in the kernel. With the table cut to 8 rounds (DASH_ARB_TABLE, read at
-    dash_create) most rounds take that path: still bit-exact vs the oracle's twin."""
-    monkeypatch.setenv("DASH_ARB_TABLE", "8")
+    its end hash their key in the kernel. With the table cut to 8 rounds (the test-only flag
+    DASH_TEST_SHORT_ARB) most rounds take that path: still bit-exact vs the oracle's twin."""
     rng = np.random.default_rng(44)
     packed, lens = random_batch(rng, 64, 8, 48, hot_frac=0.3)
-    check_batch(dash, packed, lens, 8, 4, seed=0xABCDEF)
+    check_batch(dash, packed, lens, 8, 4, seed=0xABCDEF, flags=dash.TEST_SHORT_ARB)
 
 
 def test_seeded_schedule_reaches_other_accepted_run(dash, tmp_path):

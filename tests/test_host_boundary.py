@@ -126,3 +126,16 @@ def test_bench_next_trace_text_round_trips(dash, tmp_path):
     assert f.read_text().splitlines()[:3] == ["WR 0x00 0", "WR 0x00 255", "RD 0x7F"]
     got = dash.parse_core_file(f, num_procs=8, max_instr=len(w))
     assert np.array_equal(got, np.where(w & 0x8000, w, w & 0xFF00).astype(np.uint16))
+
+
+def test_create_error_message_describes_this_call(dash, tmp_path):
+    """dash_last_error(NULL) after a failed dash_create names that call's own
+    problem, not an older handle-less failure (no device call: num_procs is checked first)."""
+    with pytest.raises(dash.DashError):
+        dash.simulate_dir(tmp_path / "missing")  # leaves a message behind
+    with pytest.raises(dash.DashError) as e:
+        dash.Engine(4, num_procs=9)
+    assert "num_procs" in str(e.value) and e.value.code == dash.EINVAL
+    with pytest.raises(dash.DashError) as e:
+        dash.Engine(4, num_procs=8, cache_size=17)
+    assert "cache_size" in str(e.value)

@@ -1,0 +1,54 @@
+"""The committed profiler evidence describes the code object that is built (CPU only).
+
+VERDICT r2 (next #2): bench.py reads roofline.traffic and the issue figures from committed
+rocprofv3 summaries (profiles/pmc_<kind>.json) and the static opcode mix from
+profiles/isa_table.json. Each records the fingerprint of sim_kernel<8,4,16,false> in the
+library it was measured on (tools/kernel_fingerprint.py: sha256 of the kernel's code and
+descriptor); they must match the library built from this tree, and the headline's traffic
+must re-derive from the one file's counters.
+"""
+import csv
+import json
+import pathlib
+import sys
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "tools"))
+import kernel_fingerprint as kf  # noqa: E402
+
+PROFILES = ROOT / "profiles"
+LIB = ROOT / "ue22cs343bb1-openmp-assignment_amd" / "libdash.so"
+
+
+@pytest.fixture(scope="module")
+def built_fp(dash):
+    return kf.fingerprint(LIB)
+
+
+@pytest.mark.parametrize("name", ["pmc_uniform.json", "pmc_contention.json", "isa_table.json"])
+def test_profile_is_of_the_built_kernel(built_fp, name):
+    prof = json.loads((PROFILES / name).read_text())
+    assert prof.get("kernel_fingerprint") == built_fp, \
+        f"{name} was measured on {prof.get('kernel_fingerprint')}, the built kernel is {built_fp}: refresh it"
+
+
+@pytest.mark.parametrize("kind", ["uniform", "contention"])
+def test_traffic_rederives_from_the_committed_counters(kind):
+    p = json.loads((PROFILES / f"pmc_{kind}.json").read_text())
+    # MI355X_MICROARCH.md HBM section: every L2->fabric read is counted by request size
+    read = p["tcc_ea0_rdreq_128b_sum"] * 128 + p["tcc_ea0_rdreq_64b_sum"] * 64 + p["tcc_ea0_rdreq_32b_sum"] * 32
+    assert read == pytest.approx(p["read_bytes_per_launch"])
+    assert p["write_size"] * 1024 == pytest.approx(p["write_bytes_per_launch"])
+    assert read + p["write_size"] * 1024 == pytest.approx(p["hbm_bytes_per_launch"])
+
+
+def test_uniform_kernel_stats_agree_with_the_pmc_run():
+    """profiles/r03/kernel_stats_uniform.csv: rocprofv3 --kernel-trace --stats of the bench command
+    with the contention leg off, so its sim_kernel<8,4,16,false> average is the headline kernel's."""
+    rows = list(csv.DictReader((PROFILES / "r03" / "kernel_stats_uniform.csv").open()))
+    row = next(r for r in rows if "sim_kernel<8, 4, 16u, false>" in r["Name"])
+    avg_ms = float(row["AverageNs"]) / 1e6
+    pmc = json.loads((PROFILES / "pmc_uniform.json").read_text())
+    assert avg_ms == pytest.approx(pmc["kernel_ms"], rel=0.03)

@@ -15,6 +15,9 @@ timeout -k 10 400 python3 bench.py --steps 10 --warmup 2 > "$OUT/bench_uniform.j
 step kernel trace
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --contention-steps 2 > "$OUT/trace.log" 2>&1 || exit 1
+step kernel trace, uniform launches only "(the headline kernel's own average)"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_uniform" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --contention-steps 0 > "$OUT/trace_uniform.log" 2>&1 || exit 1
 pmc() {  # kind name counters...
   local kind=$1 name=$2; shift 2
   step pmc "$kind" "$name"

@@ -170,7 +170,9 @@ def main():
         print(f"  {n:4d}  {op:28s} {unit({'op': op}):22s} {rate(op) if op.startswith('v_') else ''}")
     if "--json" in sys.argv:
         import json
-        out = {"kernel": sym, "rounds_per_trip": r, "source": "tools/isa_table.py (static, round loop "
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        import kernel_fingerprint
+        out = {"kernel": sym, "kernel_fingerprint": kernel_fingerprint.fingerprint(lib, sym), "rounds_per_trip": r, "source": "tools/isa_table.py (static, round loop "
                "without its waterfall loops)", "per_round": {k: tab[k] / r for k in order if tab[k]},
                "valu_rate_class_per_round": {k: rates[k] / r for k in ("full", "full*", "half", "half*")},
                "valu_full_fraction": nf / max(nf + nh, 1),

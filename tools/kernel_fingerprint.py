@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""Fingerprint of one kernel's machine code inside libdash.so (measurement infrastructure).
+
+Binds committed profiler evidence (profiles/pmc_*.json, profiles/isa_table.json) to the code
+object it was measured on: the fingerprint is sha256 over the kernel's .text bytes and its
+kernel descriptor (`<sym>.kd`: register counts, LDS size), taken from the gfx950 code object
+of the library's clang offload bundle. bench.py recomputes it from the library it runs and
+reports traffic / issue figures only when it matches.
+
+Pure Python (ELF64 + offload-bundle parsing), so it runs wherever bench.py runs.
+Usage: python3 tools/kernel_fingerprint.py [libdash.so] [symbol]
+"""
+import hashlib
+import pathlib
+import struct
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+LIB = ROOT / "ue22cs343bb1-openmp-assignment_amd" / "libdash.so"
+HEADLINE_SYM = "_ZN4dash10sim_kernelILi8ELi4ELj16ELb0EEEvNS_7SimArgsE"  # sim_kernel<8, 4, 16, false>
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def code_object(lib_bytes, arch="gfx950"):
+    """The device ELF for `arch` from the (uncompressed) clang offload bundle."""
+    base = lib_bytes.find(BUNDLE_MAGIC)
+    if base < 0:
+        raise ValueError("no clang offload bundle in the library")
+    n = struct.unpack_from("<Q", lib_bytes, base + 24)[0]
+    p = base + 32
+    for _ in range(n):
+        off, size, tlen = struct.unpack_from("<QQQ", lib_bytes, p)
+        triple = lib_bytes[p + 24:p + 24 + tlen].decode()
+        p += 24 + tlen
+        if triple.endswith(arch):
+            return lib_bytes[base + off:base + off + size]
+    raise ValueError(f"no {arch} code object in the bundle")
+
+
+def symbol_bytes(elf, name):
+    """Bytes of symbol `name` (st_value/st_size, mapped through its section) in an ELF64."""
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:
+        raise ValueError("not an ELF64 code object")
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", elf, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + i * shentsize) for i in range(shnum)]
+    for sh in secs:
+        if sh[1] != 2:  # SHT_SYMTAB
+            continue
+        strtab = secs[sh[6]]
+        for k in range(sh[5] // 24):
+            st_name, _info, _other, shndx, value, size = struct.unpack_from("<IBBHQQ", elf, sh[4] + k * 24)
+            s = elf[strtab[4] + st_name:elf.index(b"\0", strtab[4] + st_name)].decode()
+            if s == name:
+                sec = secs[shndx]
+                off = sec[4] + (value - sec[3])
+                return elf[off:off + size]
+    raise KeyError(name)
+
+
+def fingerprint(lib=LIB, sym=HEADLINE_SYM):
+    co = code_object(pathlib.Path(lib).read_bytes())
+    h = hashlib.sha256()
+    h.update(symbol_bytes(co, sym))
+    h.update(symbol_bytes(co, sym + ".kd"))
+    return h.hexdigest()[:16]
+
+
+if __name__ == "__main__":
+    args = sys.argv[1:]
+    print(fingerprint(args[0] if args else LIB, args[1] if len(args) > 1 else HEADLINE_SYM))

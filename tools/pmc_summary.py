@@ -8,12 +8,20 @@ counters were collected (tcc1 pass) the read bytes are the size-weighted sum
 RDREQ_128B x 128 + RDREQ_64B x 64 + RDREQ_32B x 32 (disjoint on this part: the
 uniform launch measured RDREQ 3.038e9 = 128B 3.038e9 + 64B 2.5e4 + 32B 0);
 otherwise 2 x FETCH_SIZE. WRITE_SIZE is taken as measured (KiB).
+The summary records the fingerprint of the headline kernel in the library the passes ran
+(tools/kernel_fingerprint.py; $DASH_LIB or the in-tree libdash.so): bench.py uses the file only
+for that code object.
 Usage: python tools/pmc_summary.py KIND KERNEL_SUBSTRING OUT_JSON DIR [DIR ...]"""
 import collections
 import csv
 import glob
 import json
+import os
+import pathlib
 import sys
+
+sys.path.insert(0, str(pathlib.Path(__file__).resolve().parent))
+import kernel_fingerprint  # noqa: E402
 
 kind, kname, out = sys.argv[1], sys.argv[2], sys.argv[3]
 agg = collections.defaultdict(float)
@@ -25,7 +33,8 @@ for d in sys.argv[4:]:
                 continue
             agg[row["Counter_Name"]] += float(row["Counter_Value"])
             dur[row["Counter_Name"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
-res = {"kernel": kname, "workload": kind, "source": " ".join(sys.argv[4:])}
+res = {"kernel": kname, "workload": kind, "source": " ".join(sys.argv[4:]),
+       "kernel_fingerprint": kernel_fingerprint.fingerprint(os.environ.get("DASH_LIB") or kernel_fingerprint.LIB)}
 for k in sorted(agg):
     res[k.lower()] = agg[k]
 read = None

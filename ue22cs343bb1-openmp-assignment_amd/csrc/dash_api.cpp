@@ -92,6 +92,8 @@ static hipError_t reset_hint(dash_t* h) {
 extern "C" {
 
 // message of the last failed handle-less call (dash_create, dash_run_host_batched) on this thread
+// largest round cap: event words carry the round in bits 30..0 (bit 31 = issued instruction)
+static constexpr uint64_t MAX_ROUNDS_CAP = 0x7FFFFFFCull;
 static thread_local char g_msg[256] = "";
 
 static void set_global_msg(const char* m) { snprintf(g_msg, sizeof g_msg, "%s", m ? m : ""); }
@@ -134,22 +136,31 @@ void dash_destroy(dash_t* h) {
 }
 
 int dash_create(const dash_cfg* cfg, dash_t** out) {
-    if (!cfg || !out) return DASH_EINVAL;
+    set_global_msg("");  // dash_last_error(NULL) describes this call only
+    auto invalid = [](const char* why) {
+        set_global_msg(why);
+        return DASH_EINVAL;
+    };
+    if (!cfg || !out) return invalid("dash_create: null cfg or out");
     *out = nullptr;
     const uint32_t N = cfg->num_procs, CS = cfg->cache_size;
-    if (N < 1 || N > DASH_MAX_PROCS) return DASH_EINVAL;
-    if (CS < 1 || CS > DASH_MAX_CACHE) return DASH_EINVAL;  // any CACHE_SIZE 1..16 (ref :7)
-    if (cfg->max_instr > (1u << 24)) return DASH_EINVAL;
-    if (cfg->num_systems > 0xFFFFFFFFull) return DASH_EINVAL;  // system ids are u32 in the lists
+    if (N < 1 || N > DASH_MAX_PROCS) return invalid("dash_create: num_procs must be 1..8");
+    if (CS < 1 || CS > DASH_MAX_CACHE) return invalid("dash_create: cache_size must be 1..16");  // (ref :7)
+    if (cfg->max_instr > (1u << 24)) return invalid("dash_create: max_instr above 2^24");
+    if (cfg->num_systems > 0xFFFFFFFFull)  // system ids are u32 in the lists
+        return invalid("dash_create: num_systems above 2^32 - 1");
     if (cfg->trace_events && (double)cfg->num_systems * N * cfg->trace_events * 8.0 > 64.0 * (1ull << 30))
-        return DASH_EINVAL;  // event log larger than 64 GiB
+        return invalid("dash_create: event log larger than 64 GiB");
     dash_t* h = new (std::nothrow) dash_ctx();
-    if (!h) return DASH_ENOMEM;
+    if (!h) {
+        set_global_msg("dash_create: out of host memory");
+        return DASH_ENOMEM;
+    }
     h->cfg = *cfg;
     if (h->cfg.max_rounds == 0) h->cfg.max_rounds = 1024ull + 256ull * cfg->max_instr;
-    // checked at the first round of every WCHUNK-round trip of the kernel: a multiple of 4
-    h->cfg.max_rounds = (h->cfg.max_rounds + 3) & ~3ull;
-    if (h->cfg.max_rounds > 0xFFFFFFFCull) h->cfg.max_rounds = 0xFFFFFFFCull;
+    // clamped below 2^31 (event words keep the round in bits 30..0) before it is rounded up to
+    // the multiple of 4 the kernel tests at the first round of every trip (no wrap to 0)
+    h->cfg.max_rounds = (std::min<uint64_t>(h->cfg.max_rounds, MAX_ROUNDS_CAP) + 3) & ~3ull;
     h->seg = next_pow2(N);
     const uint64_t spw = 64 / h->seg;
     h->groups = (cfg->num_systems + spw - 1) / spw;
@@ -171,11 +182,12 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         delete h;
+        set_global_msg("dash_create: no HIP device");
         return DASH_EDEVICE;
     }
     if (cfg->device < 0 || cfg->device >= ndev) {
         delete h;
-        return DASH_EINVAL;
+        return invalid("dash_create: device ordinal out of range");
     }
     chk(hipSetDevice(cfg->device), "hipSetDevice");
     chk(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), "hipStreamCreate");
@@ -204,9 +216,9 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
         chk(hipMalloc(&h->d_event_count, std::max<uint64_t>(nsys * N, 1) * 4), "hipMalloc(event_count)");
     }
     if (cfg->schedule_seed) {  // the seeded schedule's round words, built once per handle
-        // DASH_ARB_TABLE (tests only) shortens the table so the in-kernel hashing past its end runs
-        const char* e = getenv("DASH_ARB_TABLE");
-        const uint64_t cap = e ? (strtoull(e, nullptr, 0) & ~3ull) : dash::ARB_TABLE_MAX;
+        // DASH_TEST_SHORT_ARB (tests only) cuts the table to 8 rounds so the in-kernel hashing
+        // past its end runs
+        const uint64_t cap = (cfg->flags & DASH_TEST_SHORT_ARB) ? 8u : dash::ARB_TABLE_MAX;
         h->arb_len = (uint32_t)std::min<uint64_t>(h->cfg.max_rounds, std::min<uint64_t>(cap, dash::ARB_TABLE_MAX));
         chk(hipMalloc(&h->d_arb, ((uint64_t)h->arb_len + 4) * sizeof(uint32_t)), "hipMalloc(arb)");
         if (rc == DASH_OK) chk(dash::launch_arb_table(cfg->schedule_seed, h->seg, h->d_arb, h->arb_len, h->stream),

@@ -318,9 +318,6 @@ void sim_kernel(const SimArgs a) {
     // seeded schedule: this trip's four round words, and the next trip's (in flight)
     uint4 arbw = make_uint4(0, 0, 0, 0), arbn = make_uint4(0, 0, 0, 0);
     if (SLOW && a.arb_seed && a.arb_len) arbn = *reinterpret_cast<const uint4*>(a.arb_tab);
-#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU) || defined(DASH_PAD_VHALF)
-    uint32_t padv[4] = {lane, lane + 1, lane + 2, lane + 3}, pads[4] = {0, 1, 2, 3};
-#endif
 
     // Every predicate of a step is a wave-wide lane mask (an SGPR pair): one compare makes
     // it, the scalar unit combines them, v_cndmask consumes them. The kernel is bound by
@@ -408,22 +405,6 @@ void sim_kernel(const SimArgs a) {
         __hip_atomic_fetch_add(&lds[L::HST + pty * L::HSTRIDE + lane / P], 1u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
 
-#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU) || defined(DASH_PAD_VHALF)  // issue-cost probes (tools/ only)
-        {
-#ifdef DASH_PAD_VHALF  // 3-operand VALU (v_bfe_u32: 4 cycles per wave64 on a SIMD in tools/micro/valu_ops)
-            asm volatile(".rept %4\n v_bfe_u32 %0, %0, 1, 30\n v_bfe_u32 %1, %1, 1, 30\n v_bfe_u32 %2, %2, 1, 30\n v_bfe_u32 %3, %3, 1, 30\n .endr"
-                         : "+v"(padv[0]), "+v"(padv[1]), "+v"(padv[2]), "+v"(padv[3]) : "i"(DASH_PAD_VHALF / 4));
-#endif
-#ifdef DASH_PAD_VALU
-            asm volatile(".rept %4\n v_add_u32 %0, 1, %0\n v_add_u32 %1, 1, %1\n v_add_u32 %2, 1, %2\n v_add_u32 %3, 1, %3\n .endr"
-                         : "+v"(padv[0]), "+v"(padv[1]), "+v"(padv[2]), "+v"(padv[3]) : "i"(DASH_PAD_VALU / 4));
-#endif
-#ifdef DASH_PAD_SALU
-            asm volatile(".rept %4\n s_add_u32 %0, 1, %0\n s_add_u32 %1, 1, %1\n s_add_u32 %2, 1, %2\n s_add_u32 %3, 1, %3\n .endr"
-                         : "+s"(pads[0]), "+s"(pads[1]), "+s"(pads[2]), "+s"(pads[3]) : "i"(DASH_PAD_SALU / 4));
-#endif
-        }
-#endif
         // ---- 13-way dispatch (ref :190-618) + issue (ref :662-735), straight-line ----
         const mask_t mRR = M(pty == T_RR), mWRQ = M(pty == T_WRQ);
         const mask_t mRRD = M(pty == T_RRD), mRWR = M(pty == T_RWR);
@@ -739,9 +720,6 @@ void sim_kernel(const SimArgs a) {
         a.errors[sys] = serr;
     }
     if (live && t == 0 && handoff) a.ovf_list[atomicAdd(a.ovf_count, 1u)] = (uint32_t)sys;
-#if defined(DASH_PAD_VALU) || defined(DASH_PAD_SALU)
-    if (padv[0] + padv[1] + padv[2] + padv[3] + pads[0] + pads[1] + pads[2] + pads[3] == 0x7FFFFFFFu) a.stats[31] = 1;
-#endif
     if (a.events && report) a.event_count[sys * N + t] = nev;
     maxd >>= 8;  // ring-slot bytes -> messages
     if (a.state && report) {
@@ -890,9 +868,6 @@ static hipError_t launch_sim_p(const SimArgs& a, uint32_t cs, uint32_t ring, uin
 hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring, uint64_t groups,
                       hipStream_t s) {
     if (groups == 0) return hipSuccess;
-#ifdef DASH_HEADLINE_ONLY  // quick experiment builds (tools/): the headline kernels only
-    return seg == 8 && cs == 4 ? launch_sim_pc<8, 4>(a, ring, groups, s) : hipErrorInvalidValue;
-#else
     switch (seg) {
     case 1: return launch_sim_p<1>(a, cs, ring, groups, s);
     case 2: return launch_sim_p<2>(a, cs, ring, groups, s);
@@ -900,7 +875,6 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring
     case 8: return launch_sim_p<8>(a, cs, ring, groups, s);
     default: return hipErrorInvalidValue;
     }
-#endif
 }
 
 __global__ __launch_bounds__(256) void arb_table_kernel(uint64_t seed, uint32_t P, uint32_t* out, uint32_t n) {

@@ -42,6 +42,7 @@ EV_MSG, EV_INSTR = 0, 1
 ERR_OVERFLOW, ERR_OOB, ERR_CTZ0, ERR_DEADLOCK, ERR_ROUNDCAP, ERR_STUCK = 1, 2, 4, 8, 16, 32
 KEEP_STATE = 1
 TIER_FROM_32, TIER_FROM_256 = 2, 4
+TEST_SHORT_ARB = 8  # testing only (dash.h)
 NUM_TIERS = 3
 GEN_UNIFORM, GEN_CONTENTION, GEN_LOCALITY = 0, 1, 2
 

@@ -144,40 +144,54 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
                     lines.append(f"WR {a:02X} {v}\n" if w & 0x8000 else f"RD {a:02X}\n")
                 (d / "tests" / "b" / f"core_{n}.txt").write_text("".join(lines))
             dirs.append(d)
-        batches, t0 = 0, time.perf_counter()
+        # The reference can stall for good under some thread schedules (e.g. its undefined
+        # __builtin_ctz(0), ref :209,451, sends to "node 32", which the patch drops, and the
+        # requester then waits forever). An instance still running well after the batch's others
+        # finished (4x the slowest finisher, at least 5 s; or --ref-timeout) is killed and not
+        # counted: instructions and time are those of the instances that finished.
+        batches, hung, instr, elapsed, t0 = 0, 0, 0, 0.0, time.perf_counter()
         while True:
             procs = [subprocess.Popen([str(exe), "b"], cwd=d, stdout=subprocess.DEVNULL) for d in dirs]
-            tb, last = time.perf_counter(), time.perf_counter()
-            while any(p.poll() is None for p in procs):  # spinning instances can take minutes
-                time.sleep(0.02)
+            tb = last = time.perf_counter()
+            fin = {}
+            while len(fin) < k:
+                time.sleep(0.005)
                 now = time.perf_counter()
-                if now - tb > args.ref_timeout:
-                    for p in procs:
-                        p.kill()
-                    for p in procs:
-                        p.wait()
-                    raise RuntimeError(f"reference instances did not finish within {args.ref_timeout:.0f} s")
+                for i, p in enumerate(procs):
+                    if i not in fin and p.poll() is not None:
+                        if p.returncode != 0:
+                            raise RuntimeError(f"reference instance exited with {p.returncode}")
+                        fin[i] = now - tb
+                limit = max(5.0, 4 * max(fin.values())) if fin else args.ref_timeout
+                if len(fin) < k and now - tb > min(limit, args.ref_timeout):
+                    for i, p in enumerate(procs):
+                        if i not in fin:
+                            p.kill()
+                            p.wait()
+                            hung += 1
+                    break
                 if now - last > 30:
                     last = now
-                    print(f"[ref_baseline] {sum(p.poll() is not None for p in procs)}/{k} instances done, "
-                          f"{now - tb:.0f} s", file=sys.stderr, flush=True)
-            if any(p.returncode != 0 for p in procs):
-                raise RuntimeError(f"reference instance exited with {[p.returncode for p in procs]}")
+                    print(f"[ref_baseline] {len(fin)}/{k} instances done, {now - tb:.0f} s", file=sys.stderr,
+                          flush=True)
+            if not fin:
+                raise RuntimeError(f"no reference instance finished within {args.ref_timeout:.0f} s")
+            for i in fin:  # the instance reached quiescence and dumped its 8 nodes
+                assert all((dirs[i] / f"core_{n}_output.txt").exists() for n in range(8)), dirs[i]
             batches += 1
-            elapsed = time.perf_counter() - t0
-            if elapsed >= target_s:
+            instr += len(fin) * 8 * args.len
+            elapsed += max(fin.values())
+            if time.perf_counter() - t0 >= target_s:
                 break
-        for d in dirs:  # every instance reached quiescence and dumped its 8 nodes
-            assert all((d / f"core_{n}_output.txt").exists() for n in range(8)), d
-    instr = batches * k * 8 * args.len
     cores = host_cores()
     loc = f", locality {locality / 65536:g}" if kind_name == "locality" else ""
     return {"value": instr / elapsed, "unit": "instr/s", "cores": cores, "host_cpus_visible": host_cpus_visible(),
             "kind": "reference", "mode": "A" if k == cores else ("B" if k == 1 else f"{k} instances"),
-            "instances": k, "threads_per_instance": 8, "cpu_model": cpu_model(),
+            "instances": k, "threads_per_instance": 8, "hung_instances_killed": hung, "cpu_model": cpu_model(),
             "sample": f"{batches} batch(es) x {k} concurrent instance(s) x 8 OpenMP threads, one 8-node system "
                       f"x {args.len} instr each ({kind_name}{loc}, CS={cache_size}, systems 0..{k - 1} of seed "
-                      f"0x{seed:X}) in {elapsed:.1f} s; {cores} CPUs of cgroup quota on a host exposing "
+                      f"0x{seed:X}) in {elapsed:.1f} s ({hung} stalled instance(s) killed, not counted); {cores} "
+                      f"CPUs of cgroup quota on a host exposing "
                       f"{host_cpus_visible()} logical CPUs ({cpu_model()}); assignment.c + benchmark patch "
                       f"(oracle/patch_ref.py), gcc -O2 -fopenmp"}
 
@@ -259,6 +273,9 @@ def sweep(args, dash, rank, world, dev):
                                           stats["dropped"]] + dsum, torch.device("cuda", dev), world)
             eng.close()
             avg_s = sum(kms) / len(kms) / 1e3
+            if rank == 0:  # progress (a long silent run looks hung)
+                print(f"[sweep] CS {cs} locality {p}: {elapsed / args.steps * 1e3:.1f} ms/step", file=sys.stderr,
+                      flush=True)
             points.append({"cache_size": cs, "locality": p,
                            "value": world * M * 8 * args.len * args.steps / elapsed,
                            "ms_per_step": elapsed / args.steps * 1e3,
@@ -280,6 +297,8 @@ def sweep(args, dash, rank, world, dev):
             pt["cpu_baseline"], pt["vs_baseline"], pt["cpu_baseline_note"] = None, None, None
             if args.no_cpu_baseline:
                 continue
+            print(f"[sweep] reference baseline CS {pt['cache_size']} locality {pt['locality']}", file=sys.stderr,
+                  flush=True)
             try:
                 cpu = ref_baseline(args, args.seed, dash.GEN_LOCALITY, args.sweep_cpu_seconds, args.ref_instances,
                                    cache_size=pt["cache_size"], locality=int(round(pt["locality"] * 65536)),

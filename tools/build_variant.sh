@@ -15,7 +15,7 @@ if [ -n "${PATCHES:-}" ]; then
     for p in $PATCHES; do patch -s "$TMP/dash_kernels.hip" "$ROOT/$p"; done
     SRC=$TMP/dash_kernels.hip
 fi
-$HIPCC --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -I"$PKG/csrc" -Wno-bitwise-instead-of-logical \
+$HIPCC --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I"$ROOT/include" -I"$PKG/csrc" -Wno-bitwise-instead-of-logical -Wno-pass-failed \
     -DDASH_WAVES_PER_EU=5 "$@" -c -o "$OUT/k_$NAME.o" "$SRC"
 $HIPCC --offload-arch=gfx950 -shared -fPIC -o "$OUT/libdash_$NAME.so" "$OUT/k_$NAME.o" "$PKG/build/dash_api.o" "$PKG/build/dash_host.o"
 rm -f "$OUT/k_$NAME.o"

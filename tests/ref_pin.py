@@ -177,6 +177,8 @@ def mutant_kills(cases, max_states=MAX_STATES):
     """For every mutant oracle: the first case (in order) whose COMPLETE legal outcome set under
     the mutant misses an outcome the reference produced, or None if the mutant survives."""
     from concurrent.futures import ThreadPoolExecutor
+    if not all((MUT_DIR / f"libdash_oracle_m{k}.so").exists() for k in MUTANTS):
+        subprocess.run(["make", "-s", "-C", str(oc.ORACLE_DIR), "mutants"], check=True)
     kills = {}
     for k in MUTANTS:
         L = oc.bind(MUT_DIR / f"libdash_oracle_m{k}.so")

@@ -825,21 +825,12 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
     }
 }
 
-// occupancy experiments only (tools/): DASH_LDS_PAD adds dynamic LDS per workgroup
-static uint32_t lds_pad() {
-    static const uint32_t pad = [] {
-        const char* e = getenv("DASH_LDS_PAD");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    return pad;
-}
-
 template <int P, int CS, uint32_t RING>
 static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t s) {
     if (a.arb_seed || a.events)
-        hipLaunchKernelGGL((sim_kernel<P, CS, RING, true>), dim3((uint32_t)groups), dim3(64), lds_pad(), s, a);
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, true>), dim3((uint32_t)groups), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((sim_kernel<P, CS, RING, false>), dim3((uint32_t)groups), dim3(64), lds_pad(), s, a);
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, false>), dim3((uint32_t)groups), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

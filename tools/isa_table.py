@@ -166,7 +166,7 @@ def main():
     nh = rates["half"] + rates["half*"]
     print(f"  pipe model: {nf / r:.1f} x 2 + {nh / r:.1f} x 4 = {(2 * nf + 4 * nh) / r:.0f} SIMD cycles per round")
     print("\ntop opcodes (per trip):")
-    for op, n in ops.most_common(24):
+    for op, n in ops.most_common(int(os.environ.get("ISA_TOP", "24"))):
         print(f"  {n:4d}  {op:28s} {unit({'op': op}):22s} {rate(op) if op.startswith('v_') else ''}")
     if "--json" in sys.argv:
         import json

@@ -9,6 +9,8 @@ oracle's run of the same traces (oracle/dash_oracle.c). Three of
 cases have systems whose queues outgrow the 16-deep first tier (case 1: about 14 % of its
 systems, depth up to 23), so tier hand-offs happen inside mixed waves; the tier-256 path has
 its own tests in test_gpu_parity.py."""
+import os
+
 import numpy as np
 import pytest
 
@@ -16,16 +18,20 @@ from oracle_ctypes import run_system
 from test_gpu_parity import random_batch
 
 pytestmark = pytest.mark.gpu
-CASES = 32
+# a longer campaign with other seeds: DASH_FUZZ_CASES=400 DASH_FUZZ_BASE=5000 (the suite's
+# default is the 32 cases from seed 1000); DASH_FUZZ_MAXLEN raises the longest trace
+CASES = int(os.environ.get("DASH_FUZZ_CASES", "32"))
+BASE = int(os.environ.get("DASH_FUZZ_BASE", "1000"))
+MAXLEN = int(os.environ.get("DASH_FUZZ_MAXLEN", "600"))
 NSYS = 2048
 
 
 @pytest.mark.parametrize("case", range(CASES))
 def test_fuzz_batch_matches_oracle(dash, case):
-    rng = np.random.default_rng(1000 + case)
+    rng = np.random.default_rng(BASE + case)
     N = int(rng.integers(1, 9))
     CS = int(rng.integers(1, 17))
-    L = int(rng.integers(1, 601))
+    L = int(rng.integers(1, MAXLEN + 1))
     span = int(rng.choice([4, 16]))
     hot = float(rng.choice([0.0, 0.0, 0.5, 0.9]))
     seed = int(rng.integers(1, 1 << 31)) if case % 4 == 3 else 0

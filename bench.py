@@ -248,7 +248,7 @@ def read_profile(kind, fp):
         return None, f"{f.relative_to(ROOT)} unreadable: {e}"
     if fp is None or prof.get("kernel_fingerprint") != fp:
         return None, (f"{f.relative_to(ROOT)} was measured on kernel {prof.get('kernel_fingerprint')}, this run's "
-                      f"sim_kernel<8,4,16,false> is {fp}: its counters do not describe this binary, so traffic "
+                      f"sim_kernel<8,4,16,0> is {fp}: its counters do not describe this binary, so traffic "
                       f"and issue figures are omitted")
     return prof, None
 

@@ -15,7 +15,7 @@ n = sys.argv[1]
 agg = collections.defaultdict(float); dur = 0
 for f in glob.glob(f"gpurun_out/abp/{n}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "sim_kernel<8, 4, 16u, false>" in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in ("sim_kernel<8, 4, 16u, false>", "sim_kernel<8, 4, 16u, 0>")):
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
 wr = json.load(open(f"gpurun_out/abp/{n}.log".replace(".log", ".log")) if False else None) if False else None

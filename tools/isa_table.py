@@ -2,7 +2,7 @@
 """Instruction table of the round loop of the headline kernel.
 
 Disassembles the gfx950 code object inside libdash.so, finds the round loop of
-sim_kernel<8, 4, 16, false> (the tightest backward branch around four arrival exchanges) and counts its
+sim_kernel<8, 4, 16, 0> (the tightest backward branch around four arrival exchanges) and counts its
 instructions by encoding and unit: VOP1/VOP2/VOPC in their 32-bit forms, VOP3 (64-bit
 encodings: three-operand ops, SGPR-mask selects and compares, modifiers), SDWA, SALU, LDS,
 VMEM, branches, waits. Counts are static, over one trip of the loop (DASH_QCHECK = 4
@@ -25,7 +25,7 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
-SYM = "_ZN4dash10sim_kernelILi8ELi4ELj16ELb0EEEvNS_7SimArgsE"
+SYM = "_ZN4dash10sim_kernelILi8ELi4ELj16ELi0EEEvNS_7SimArgsE"
 ROUNDS_PER_TRIP = 4
 
 # measured in tools/micro/valu_ops.hip (32 waves/CU, profiles/r01/micro/valu_ops.txt and

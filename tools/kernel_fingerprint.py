@@ -21,7 +21,8 @@ import sys
 
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 LIB = ROOT / "ue22cs343bb1-openmp-assignment_amd" / "libdash.so"
-HEADLINE_SYM = "_ZN4dash10sim_kernelILi8ELi4ELj16ELb0EEEvNS_7SimArgsE"  # sim_kernel<8, 4, 16, false>
+HEADLINE_SYM = "_ZN4dash10sim_kernelILi8ELi4ELj16ELi0EEEvNS_7SimArgsE"  # sim_kernel<8, 4, 16, 0> (the lockstep mode;
+# sim_kernel<8, 4, 16, false> before round 3 session 2, same bytes)
 BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 

@@ -39,7 +39,7 @@ struct dash_ctx {
     uint32_t* d_list[2] = {nullptr, nullptr};  // overflow hand-off lists (ping-pong)
     uint32_t* d_count = nullptr;
     uint32_t* d_events = nullptr;       // [(sys*N+node)*trace_events][2]
-    uint32_t* d_arb = nullptr;          // seeded schedule: one word per round (dash::arb_word)
+    uint32_t* d_arb = nullptr;          // seeded schedule: one word per node and round (dash::arb_node)
     uint32_t arb_len = 0;
     uint32_t* d_event_count = nullptr;  // [sys*N+node]
     uint64_t tier_systems[dash::NUM_TIERS] = {};  // systems run per queue-depth tier, last run
@@ -220,7 +220,7 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
         // past its end runs
         const uint64_t cap = (cfg->flags & DASH_TEST_SHORT_ARB) ? 8u : dash::ARB_TABLE_MAX;
         h->arb_len = (uint32_t)std::min<uint64_t>(h->cfg.max_rounds, std::min<uint64_t>(cap, dash::ARB_TABLE_MAX));
-        chk(hipMalloc(&h->d_arb, ((uint64_t)h->arb_len + 4) * sizeof(uint32_t)), "hipMalloc(arb)");
+        chk(hipMalloc(&h->d_arb, ((uint64_t)h->arb_len + 4) * h->seg * sizeof(uint32_t)), "hipMalloc(arb)");
         if (rc == DASH_OK) chk(dash::launch_arb_table(cfg->schedule_seed, h->seg, h->d_arb, h->arb_len, h->stream),
                                "arb table");
         if (rc == DASH_OK) chk(hipStreamSynchronize(h->stream), "arb table");

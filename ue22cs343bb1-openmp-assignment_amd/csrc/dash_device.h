@@ -85,8 +85,9 @@ constexpr uint32_t CHUNK_INSTR = 4;  // instructions per 8-B trace chunk
 // its last instruction (never issued), so the last lane's stream needs no bounds test
 constexpr uint64_t TRACE_PAD = 64;
 hipError_t launch_gen(const GenArgs& g, hipStream_t s);
-// the seeded schedule's per-round words (arb_word) for rounds [0, n), n a multiple of 4
-constexpr uint32_t ARB_TABLE_MAX = 1u << 24;
+// the seeded schedule's table: each node's word (arb_node) of rounds [0, n), n a multiple of 4,
+// laid out [round / 4][node < seg][round % 4]; rounds past it are hashed in sim_kernel
+constexpr uint32_t ARB_TABLE_MAX = 1u << 22;
 hipError_t launch_arb_table(uint64_t seed, uint32_t seg, uint32_t* out, uint32_t n, hipStream_t s);
 // skip[list[i]] = 1 for i < n
 // RD words carry value 0 (ref :839): clears bits 7..0 of every word whose bit 15 is 0

@@ -91,6 +91,12 @@ __device__ __forceinline__ uint32_t arb_word(uint64_t seed, uint32_t round, uint
         w |= ((((skey >> (8 * t)) & 3u) == 0 ? 1u : 0u) << t) | (((t * A + Bc) & (P - 1)) << (8 + 3 * t));
     return w;
 }
+// node t's part of a round word, as the kernel consumes it: 0 when t sits the round out,
+// else its primary arrival bit 2 << 4 * (delivery position) (the INV bit is one below it,
+// the flush copy's one above)
+__device__ __forceinline__ uint32_t arb_node(uint32_t w, uint32_t t) {
+    return ((w >> t) & 1u) ? 0u : 2u << (4u * ((w >> (8 + 3 * t)) & 7u));
+}
 
 // CS = CACHE_SIZE; CS = 0 is the generic kernel for a non-power-of-two CACHE_SIZE (read at
 // run time, LDS sized for the maximum of 16 lines)
@@ -152,17 +158,24 @@ __device__ __forceinline__ mask_t Mbit15(uint32_t v) {
 // keeps a rarely taken branch a branch (no if-conversion onto the common path)
 #define COLD() asm volatile("" ::: "memory")
 
-// SLOW: the kernel for the rarely used run options, checked at run time: a seeded legal
-// schedule (a.arb_seed != 0, DESIGN.md §2 -- per round, a node sits out with probability
-// 1/4 and senders deliver in a seeded affine order; oracle twins orc_arb_stall,
-// orc_arb_prio) and the DEBUG_MSG / DEBUG_INSTR event log (a.events). The fast kernel
-// (SLOW = false) has neither: every node steps, lowest sender first.
-template <int P, int CS, uint32_t RING, bool SLOW>
+// MODE: 0 = the fast kernel, every node steps, lowest sender first; the rarely used run
+// options get instantiations of their own, so neither they nor their kernel arguments cost
+// the fast one anything:
+//   1 = a seeded legal schedule (a.arb_seed != 0, DESIGN.md §2 -- per round, a node sits out
+//       with probability 1/4 and senders deliver in a seeded affine order; oracle twins
+//       orc_arb_stall, orc_arb_prio);
+//   2 = the DEBUG_MSG / DEBUG_INSTR event log (a.events), lockstep or seeded (tested at run
+//       time).
+// Mode 1 without the event-log code keeps its loop free of SGPR spill reloads.
+template <int P, int CS, uint32_t RING, int MODE>
 __global__ __launch_bounds__(64)
 #if DASH_WAVES_PER_EU
 __attribute__((amdgpu_waves_per_eu(DASH_WAVES_PER_EU)))
 #endif
 void sim_kernel(const SimArgs a) {
+    constexpr bool SLOW = MODE != 0;
+    // the seeded schedule is on (compile-time in modes 0 and 1)
+    const bool ARB = MODE == 1 || (MODE == 2 && a.arb_seed != 0);
     using L = Lds<P, CS, RING>;
     const uint32_t ncs = CS ? (uint32_t)CS : a.cache_size;  // cache lines per node
     constexpr uint32_t SPW = 64 / P;
@@ -315,9 +328,11 @@ void sim_kernel(const SimArgs a) {
     // the trip's first step; the step at position k of the trip is round rv + k
     uint32_t rv = 0;
     asm volatile("" : "+v"(rv));
-    // seeded schedule: this trip's four round words, and the next trip's (in flight)
+    // seeded schedule: this node's words (arb_node) of this trip's four rounds, and of the next
+    // trip's (in flight); the table holds them as [round / 4][node][4]
     uint4 arbw = make_uint4(0, 0, 0, 0), arbn = make_uint4(0, 0, 0, 0);
-    if (SLOW && a.arb_seed && a.arb_len) arbn = *reinterpret_cast<const uint4*>(a.arb_tab);
+    const uint4* const arbt = reinterpret_cast<const uint4*>(a.arb_tab) + t;
+    if (ARB && a.arb_len) arbn = arbt[0];
 
     // Every predicate of a step is a wave-wide lane mask (an SGPR pair): one compare makes
     // it, the scalar unit combines them, v_cndmask consumes them. The kernel is bound by
@@ -337,12 +352,14 @@ void sim_kernel(const SimArgs a) {
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
         mask_t mStall = 0;
         uint32_t bitI = 1u << (4 * t);
-        if (SLOW && a.arb_seed) {
-            // the round's word (wave-uniform): from the table, loaded a trip ahead, or hashed at
-            // the trip start past the table's end
-            const uint32_t w = k == 0 ? arbw.x : k == 1 ? arbw.y : k == 2 ? arbw.z : arbw.w;
-            mStall = M(((w >> t) & 1u) != 0);
-            bitI = 1u << (((w >> (8 + 3 * t)) & 7u) << 2);
+        uint32_t wp = 0;
+        if (ARB) {
+            // this node's word of the round: from the table, loaded a trip ahead, or hashed at
+            // the trip start past the table's end; 0 = the node sits the round out, else its
+            // primary arrival bit
+            wp = k == 0 ? arbw.x : k == 1 ? arbw.y : k == 2 ? arbw.z : arbw.w;
+            mStall = M(wp == 0u);
+            bitI = wp >> 1;
         }
         const mask_t mHas = mMsg & ~mStall;           // pops this round
         const mask_t mDo = mIss & ~mMsg & ~mStall;    // issues this round
@@ -388,7 +405,7 @@ void sim_kernel(const SimArgs a) {
         // the popped message's type, or 13 (no transactionType) for a lane that does not pop:
         // the type masks below then need no AND with mHas
         const uint32_t pty = B(mHas) ? mty : 13u;
-        if (SLOW && a.events) {  // wave-uniform: the batch-of-1 trace (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652)
+        if (MODE == 2) {  // the batch-of-1 trace: the batch-of-1 trace (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652)
             COLD();
             if (B(mHas | mDo)) {
                 if (nev < a.event_cap) {
@@ -531,7 +548,11 @@ void sim_kernel(const SimArgs a) {
         // compares the receiver's count plus that rank with the ring depth.
         // tail (with ring column); the final tier adds count << 16 for the capacity check
         lds[L::MQT + L::MQS * lane] = FINAL ? tq | (cq << 8) : tq;
-        const uint32_t bitP = bitI << 1, bitB = bitI << 2;
+        uint32_t bitP = bitI << 1, bitB = bitI << 2;
+        if (ARB) {
+            bitP = wp;
+            bitB = dbl(wp);
+        }
         if (B(mVP))
             __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (B(mVB))
@@ -656,14 +677,15 @@ void sim_kernel(const SimArgs a) {
             }
         }
         refill();
-        if (SLOW && a.arb_seed) {
+        if (ARB) {
             arbw = arbn;
-            if (rv + 4 < a.arb_len) arbn = *reinterpret_cast<const uint4*>(a.arb_tab + rv + 4);
+            if (rv + 4 < a.arb_len) arbn = arbt[((rv + 4) >> 2) * P];
             if (rv >= a.arb_len) {  // past the table (arb_len is a multiple of 4, like rv)
                 COLD();
                 const uint32_t r0 = __builtin_amdgcn_readfirstlane(rv);
-                arbw = make_uint4(arb_word(a.arb_seed, r0, P), arb_word(a.arb_seed, r0 + 1, P),
-                                  arb_word(a.arb_seed, r0 + 2, P), arb_word(a.arb_seed, r0 + 3, P));
+                arbw = make_uint4(arb_node(arb_word(a.arb_seed, r0, P), t), arb_node(arb_word(a.arb_seed, r0 + 1, P), t),
+                                  arb_node(arb_word(a.arb_seed, r0 + 2, P), t),
+                                  arb_node(arb_word(a.arb_seed, r0 + 3, P), t));
             }
         }
         step(0, mMsg, mIss);
@@ -827,10 +849,12 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
 
 template <int P, int CS, uint32_t RING>
 static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t s) {
-    if (a.arb_seed || a.events)
-        hipLaunchKernelGGL((sim_kernel<P, CS, RING, true>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+    if (a.events)
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, 2>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+    else if (a.arb_seed)
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, 1>), dim3((uint32_t)groups), dim3(64), 0, s, a);
     else
-        hipLaunchKernelGGL((sim_kernel<P, CS, RING, false>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, 0>), dim3((uint32_t)groups), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 
@@ -868,9 +892,12 @@ hipError_t launch_sim(const SimArgs& a, uint32_t seg, uint32_t cs, uint32_t ring
     }
 }
 
+// [round / 4][node][round % 4]: one 16-B load per node and trip in sim_kernel
 __global__ __launch_bounds__(256) void arb_table_kernel(uint64_t seed, uint32_t P, uint32_t* out, uint32_t n) {
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x)
-        out[r] = arb_word(seed, r, P);
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+        const uint32_t w = arb_word(seed, r, P);
+        for (uint32_t t = 0; t < P; ++t) out[((uint64_t)(r >> 2) * P + t) * 4 + (r & 3)] = arb_node(w, t);
+    }
 }
 
 hipError_t launch_arb_table(uint64_t seed, uint32_t seg, uint32_t* out, uint32_t n, hipStream_t s) {

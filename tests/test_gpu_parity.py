@@ -254,6 +254,27 @@ def test_debug_trace_random_batch(dash):
             assert dash.format_events(eng.read_events(s)) == log, s
 
 
+@pytest.mark.parametrize("seed", [87, 0x5EED5EED])
+def test_debug_trace_under_seeded_schedule(dash, seed):
+    """The event-log kernel (MODE 2) with a seeded schedule switched on at run time: every
+    system's formatted DEBUG_MSG / DEBUG_INSTR log equals the oracle's log of the same seeded
+    schedule, and the digests equal those of the seeded kernel without the log (MODE 1)."""
+    rng = np.random.default_rng(seed & 0xFFFF)
+    packed, lens = random_batch(rng, 24, 8, 40, block_span=4, hot_frac=0.5)
+    with dash.Engine(24, num_procs=8, cache_size=2, max_instr=40, trace_events=512, schedule_seed=seed) as eng:
+        eng.load_traces(packed, lens)
+        eng.run()
+        dig_log = eng.read_results()[0]
+        for s in range(24):
+            _, log = run_system(packed[s], lens[s], num_procs=8, cache_size=2, log=True, log_msgs=True,
+                                arb_seed=seed)
+            assert dash.format_events(eng.read_events(s)) == log, s
+    with dash.Engine(24, num_procs=8, cache_size=2, max_instr=40, schedule_seed=seed) as eng:
+        eng.load_traces(packed, lens)
+        eng.run()
+        assert np.array_equal(eng.read_results()[0], dig_log)
+
+
 def test_debug_trace_truncation_is_reported(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4) as eng:

@@ -75,6 +75,9 @@ TARGETS += [(f"cache_simulator_bench_cs{cs}", ["-DNUM_PROCS=8", "-DMAX_INSTR_NUM
             for cs in (1, 2, 8, 16)]
 TARGETS += [(f"cache_simulator_pin_cs{cs}", ["-DNUM_PROCS=4", "-DMAX_INSTR_NUM=32", f"-DCACHE_SIZE={cs}",
                                               "-DDEBUG_MSG"]) for cs in (1, 4)]
+# the same at the headline's 8 nodes (round 3): cross-node traffic among 8 homes
+TARGETS += [(f"cache_simulator_pin8_cs{cs}", ["-DNUM_PROCS=8", "-DMAX_INSTR_NUM=32", f"-DCACHE_SIZE={cs}",
+                                               "-DDEBUG_MSG"]) for cs in (1, 4)]
 
 
 def main():

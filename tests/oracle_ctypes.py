@@ -205,7 +205,8 @@ def explore(trace, lens, num_procs=4, cache_size=4, max_states=1_000_000, max_ou
                            ctypes.addressof(states), ctypes.addressof(full))
     if rc != 0:
         raise ValueError("explore failed")
-    return [outs[k] for k in range(min(n.value, max_outs))], int(states.value), bool(full.value)
+    # more distinct outcomes than max_outs: the list is cut, so the set is not complete
+    return [outs[k] for k in range(min(n.value, max_outs))], int(states.value), bool(full.value) and n.value <= max_outs
 
 
 def dump_node(res, node, cache_size=4, L=None) -> str:

@@ -26,7 +26,8 @@ transactionType (ref :30-44), plus
   * the EVICT_SHARED hand-off: an EVICT_SHARED handled by a node that is not the address's
     home (sent by the home to the last sharer, ref :569-580).
 
-`python3 tests/ref_pin.py OUT.json` writes the coverage table (profiles/r03/ref_pin_coverage.json).
+`python3 tests/ref_pin.py OUT.json` writes the coverage table (profiles/r03/ref_pin_coverage.json);
+`--nodes 8` runs the same at the headline's node count (profiles/r03/ref_pin8_coverage.json).
 """
 from __future__ import annotations
 
@@ -46,6 +47,10 @@ import oracle_ctypes as oc  # noqa: E402
 REF_DIR = oc.ROOT / "oracle" / "_ref"
 COUNT = 208
 RUNS = 4
+# the headline's 8 nodes (oracle/_ref/cache_simulator_pin8_cs{1,4}): 2-4 nodes with instructions
+# among 8 homes, fewer runs per trace
+COUNT8 = 160
+RUNS8 = 3
 MAX_STATES = 200_000
 THREADS = 6  # explorations in parallel (ctypes drops the GIL)
 # oracle/Makefile `mutants`: one misreading of a cross-node handler each (dash_oracle.c ORC_MUTANT)
@@ -62,25 +67,26 @@ MUT_DIR = oc.ROOT / "oracle" / "_mut"
 LINE = re.compile(r"Processor (\d+) msg from: (\d+), type: (\d+), address: 0x([0-9A-F]{2})")
 
 
-def pin_exe(cs):
-    return REF_DIR / f"cache_simulator_pin_cs{cs}"
+def pin_exe(cs, n=4):
+    return REF_DIR / (f"cache_simulator_pin_cs{cs}" if n == 4 else f"cache_simulator_pin{n}_cs{cs}")
 
 
-def available():
-    return all(pin_exe(cs).exists() for cs in (1, 4))
+def available(n=4):
+    return all(pin_exe(cs, n).exists() for cs in (1, 4))
 
 
-def gen_trace(seed):
-    """(cache_size, rows) of one small cross-node 4-node system."""
+def gen_trace(seed, n=4):
+    """(cache_size, rows) of one small cross-node n-node system: 2-4 nodes with instructions,
+    homes on any of the n nodes."""
     rng = np.random.default_rng(seed)
     cs = (1, 4)[seed % 2]
-    act = rng.choice(4, int(rng.integers(2, 5)), replace=False)
+    act = rng.choice(n, int(rng.integers(2, 5)), replace=False)
     b0 = int(rng.integers(0, 16))
     blocks = [b0] if rng.random() < 0.4 else [b0, (b0 + cs * int(rng.integers(1, 16 // cs))) % 16]
-    rows = [[] for _ in range(4)]
+    rows = [[] for _ in range(n)]
     for t in act:
         for _ in range(int(rng.integers(1, 5))):
-            a = (int(rng.integers(0, 4)) << 4) | int(rng.choice(blocks))
+            a = (int(rng.integers(0, n)) << 4) | int(rng.choice(blocks))
             w = rng.random() < 0.5
             rows[t].append(oc.pack("W" if w else "R", a, int(rng.integers(1, 256)) if w else 0))
     return cs, rows
@@ -88,7 +94,7 @@ def gen_trace(seed):
 
 def as_arrays(rows):
     L = max(max(len(r) for r in rows), 1)
-    tr = np.zeros((4, L), np.uint16)
+    tr = np.zeros((len(rows), L), np.uint16)
     for n, r in enumerate(rows):
         tr[n, :len(r)] = r
     return tr, np.array([len(r) for r in rows], np.uint32)
@@ -120,7 +126,7 @@ def coverage_of(lines, cov):
         max(0, n - wbinv[k]) for k, n in fia_home.items())
 
 
-def run(count=COUNT, runs=RUNS, max_states=MAX_STATES):
+def run(count=COUNT, runs=RUNS, max_states=MAX_STATES, n=4):
     """Returns a report: per trace the legal-set size and the reference's outcomes, coverage,
     and the list of violations (reference outcome not in the complete legal set)."""
     cov = collections.Counter()
@@ -130,10 +136,10 @@ def run(count=COUNT, runs=RUNS, max_states=MAX_STATES):
     from concurrent.futures import ThreadPoolExecutor
 
     def explore(seed):
-        cs, rows = gen_trace(seed)
+        cs, rows = gen_trace(seed, n)
         tr, lens = as_arrays(rows)
-        outs, _, complete = oc.explore(tr, lens, num_procs=4, cache_size=cs, max_states=max_states)
-        legal = {tuple(oc.dump_node(o, k, cs) for k in range(4)) for o in outs} if complete else None
+        outs, _, complete = oc.explore(tr, lens, num_procs=n, cache_size=cs, max_states=max_states)
+        legal = {tuple(oc.dump_node(o, k, cs) for k in range(n)) for o in outs} if complete else None
         return seed, cs, rows, legal
 
     with tempfile.TemporaryDirectory() as td, ThreadPoolExecutor(THREADS) as pool:
@@ -151,14 +157,14 @@ def run(count=COUNT, runs=RUNS, max_states=MAX_STATES):
                 write_trace(d / "tests" / "t", rows)
                 seen = set()
                 for _ in range(runs):
-                    p = subprocess.run(["timeout", "10", str(pin_exe(cs)), "t"], cwd=d, capture_output=True,
+                    p = subprocess.run(["timeout", "10", str(pin_exe(cs, n)), "t"], cwd=d, capture_output=True,
                                        text=True)
                     report["reference_runs"] += 1
                     if p.returncode != 0:
                         report["timeouts"] += 1
                         report["violations"].append({"seed": seed, "why": f"reference exit {p.returncode}"})
                         continue
-                    got = tuple((d / f"core_{k}_output.txt").read_text() for k in range(4))
+                    got = tuple((d / f"core_{k}_output.txt").read_text() for k in range(n))
                     seen.add(got)
                     coverage_of(p.stdout, cov)
                     if got not in legal:
@@ -173,7 +179,7 @@ def run(count=COUNT, runs=RUNS, max_states=MAX_STATES):
     return report
 
 
-def mutant_kills(cases, max_states=MAX_STATES):
+def mutant_kills(cases, max_states=MAX_STATES, n=4):
     """For every mutant oracle: the first case (in order) whose COMPLETE legal outcome set under
     the mutant misses an outcome the reference produced, or None if the mutant survives."""
     from concurrent.futures import ThreadPoolExecutor
@@ -186,10 +192,10 @@ def mutant_kills(cases, max_states=MAX_STATES):
         def killed(case):
             seed, cs, rows, seen = case
             tr, lens = as_arrays(rows)
-            outs, _, complete = oc.explore(tr, lens, num_procs=4, cache_size=cs, max_states=max_states, L=L)
+            outs, _, complete = oc.explore(tr, lens, num_procs=n, cache_size=cs, max_states=max_states, L=L)
             if not complete:
                 return False
-            legal = {tuple(oc.dump_node(o, n, cs, L=L) for n in range(4)) for o in outs}
+            legal = {tuple(oc.dump_node(o, k, cs, L=L) for k in range(n)) for o in outs}
             return any(got not in legal for got in seen)
 
         kills[k] = None
@@ -204,9 +210,15 @@ def mutant_kills(cases, max_states=MAX_STATES):
 
 
 if __name__ == "__main__":
-    rep = run()
+    args = sys.argv[1:]
+    n = 4
+    if "--nodes" in args:
+        n = int(args[args.index("--nodes") + 1])
+        del args[args.index("--nodes"):args.index("--nodes") + 2]
+    count, runs = (COUNT, RUNS) if n == 4 else (COUNT8, RUNS8)
+    rep = run(count, runs, n=n)
     cases = rep.pop("cases")
-    kills = mutant_kills(cases)
+    kills = mutant_kills(cases, n=n)
     rep["mutants"] = {f"m{k}: {MUTANTS[k]}": (f"rejected: a reference outcome is not legal under it (trace seed {s})"
                                               if s is not None else "final states do not separate it")
                       for k, s in kills.items()}
@@ -217,9 +229,11 @@ if __name__ == "__main__":
     if kills.get(4) is None and dup > 0:
         rep["mutants"][f"m4: {MUTANTS[4]}"] = (f"rejected by the reference's DEBUG_MSG stream: {dup} FLUSH_INVACKs "
                                               f"handled by a home beyond one per WRITEBACK_INV it forwarded")
-    out = json.dumps({"source": "tests/ref_pin.py (oracle/_ref/cache_simulator_pin_cs{1,4}: assignment.c + "
-                                "oracle/patch_ref.py, NUM_PROCS 4, MAX_INSTR_NUM 32, -DDEBUG_MSG)",
-                      "count": COUNT, "runs_per_trace": RUNS, "max_states": MAX_STATES, **rep}, indent=1)
-    if len(sys.argv) > 1:
-        pathlib.Path(sys.argv[1]).write_text(out + "\n")
+    exe = "cache_simulator_pin_cs{1,4}" if n == 4 else f"cache_simulator_pin{n}_cs{{1,4}}"
+    out = json.dumps({"source": f"tests/ref_pin.py (oracle/_ref/{exe}: assignment.c + "
+                                f"oracle/patch_ref.py, NUM_PROCS {n}, MAX_INSTR_NUM 32, -DDEBUG_MSG)",
+                      "num_procs": n, "count": count, "runs_per_trace": runs, "max_states": MAX_STATES, **rep},
+                     indent=1)
+    if args:
+        pathlib.Path(args[0]).write_text(out + "\n")
     print(out)

@@ -43,3 +43,17 @@ def test_mutant_oracles_are_refuted(report):
     survivors = [k for k, s in kills.items() if s is None and not (k == 4 and report["coverage"][
         "WRITEBACK_INV with home == requester"] > 0)]
     assert survivors == [], {k: ref_pin.MUTANTS[k] for k in survivors}
+
+
+@pytest.mark.skipif(not ref_pin.available(8), reason="8-node reference pin binaries not built")
+def test_reference_outcomes_at_eight_nodes():
+    """The same pin at the headline's node count: the reference built with NUM_PROCS 8
+    (oracle/_ref/cache_simulator_pin8_cs{1,4}) on 160 small random systems whose 2-4 active
+    nodes address homes among all 8 nodes, 3 runs each; every dump set lies in the oracle
+    explorer's complete legal outcome set, and every handler is exercised."""
+    rep = ref_pin.run(ref_pin.COUNT8, ref_pin.RUNS8, n=8)
+    assert rep["traces"] == ref_pin.COUNT8
+    assert rep["violations"] == [], rep["violations"][:5]
+    assert rep["distinct_reference_outcomes_total"] > ref_pin.COUNT8
+    assert all(rep["coverage"][t] > 0 for t in ref_pin.oc.TXN_NAMES), rep["coverage"]
+

@@ -184,10 +184,33 @@ def seeded_row(dash, dev, seed, systems, L, steps):
     return out
 
 
+def digests_at_scale(dash, dev, seed, systems, td):
+    """dash_write_digests for a headline-sized batch (every system's digest, rounds and error
+    word as text: parity at 1M systems without 19 GB of dumps). Short traces:
+    the row times the emitter, not the simulation."""
+    L = 64
+    with dash.Engine(systems, num_procs=8, cache_size=4, max_instr=L, device=dev) as eng:
+        eng.generate(seed, L, kind=dash.GEN_UNIFORM)
+        eng.run()
+        dig, rnd, err = eng.read_results()
+        path = pathlib.Path(td, "digests_1m.txt")
+        t0 = time.perf_counter()
+        eng.write_digests(path)
+        t = time.perf_counter() - t0
+    text = path.read_bytes()
+    lines = text.split(b"\n")[:-1]
+    sample = range(0, systems, max(systems // 4096, 1))
+    ok = len(lines) == systems and all(
+        lines[k] == f"{k} {int(dig[k]):016x} {int(rnd[k])} {int(err[k]):x}".encode() for k in sample)
+    return {"systems": systems, "seconds": t, "systems_per_s": systems / t, "bytes": len(text),
+            "parity_lines_equal_results": bool(ok)}
+
+
 def run(dash, dev, args):
     L = min(args.len, 4096)
     with tempfile.TemporaryDirectory(dir=args.next_dir) as td:
         res, packed, lens = ingest_rows(dash, dev, args.seed, args.next_systems, L, td)
+        res["digests"]["at_scale"] = digests_at_scale(dash, dev, args.seed, args.systems, td)
     res["events"] = events_row(dash, dev, args.seed, args.next_event_systems, L)
     res["seeded"] = seeded_row(dash, dev, args.seed, args.systems, args.len, max(args.steps, 1))
     line = {"metric": "SURVEY.md 8(f) rows beside the hot path (ingest, digests/dumps, DEBUG events, seeded schedules)",

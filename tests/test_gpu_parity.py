@@ -338,6 +338,21 @@ def test_bulk_dirs_ingest_and_dump(dash, tmp_path):
         assert int(sysid) == k and int(dig, 16) == run_system(tr, lens).digest
 
 
+def test_digest_file_is_the_results_formatted(dash, tmp_path):
+    """dash_write_digests (parallel hand-formatted chunks) writes exactly the lines
+    "%llu %016llx %u %x" of dash_read_results for every system, across chunk boundaries
+    (65,536 lines) and with nonzero error words (uniform traces send to node 15, ref :772)."""
+    n = 70_000
+    with dash.Engine(n, num_procs=8, cache_size=4, max_instr=48) as eng:
+        eng.generate(0x5EED, 48, kind=dash.GEN_UNIFORM)
+        eng.run()
+        dig, rnd, err = eng.read_results()
+        eng.write_digests(tmp_path / "d.txt")
+    assert int((err != 0).sum()) > 0
+    exp = "".join(f"{k} {int(dig[k]):016x} {int(rnd[k])} {int(err[k]):x}\n" for k in range(n))
+    assert (tmp_path / "d.txt").read_text() == exp
+
+
 def test_cli_batch_and_synthetic(dash, tmp_path):
     exe = dash.PKG / "cache_simulator"
     lst = tmp_path / "dirs.txt"

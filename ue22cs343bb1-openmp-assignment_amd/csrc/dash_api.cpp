@@ -627,9 +627,47 @@ int dash_write_digests(dash_t* h, const char* path) {
     if (rc != DASH_OK) return rc;
     FILE* f = fopen(path, "w");
     if (!f) return fail(h, DASH_EIO, "open %s", path);
-    for (uint64_t k = 0; k < n; k++)
-        fprintf(f, "%llu %016llx %u %x\n", (unsigned long long)k, (unsigned long long)d[k], r[k], e[k]);
-    return fclose(f) == 0 ? DASH_OK : fail(h, DASH_EIO, "write %s", path);
+    // the lines of fprintf("%llu %016llx %u %x\n"), formatted by hand in parallel chunks (one
+    // fprintf per line ran at ~4e6 lines/s) and written in order
+    constexpr uint64_t CHUNK = 1u << 16;  // lines per chunk: <= 64 B each
+    const uint64_t nch = (n + CHUNK - 1) / CHUNK;
+    std::vector<std::vector<char>> buf(nch);
+    std::atomic<uint64_t> next{0};
+    auto work = [&] {
+        static const char HEX[] = "0123456789abcdef";
+        for (uint64_t c; (c = next.fetch_add(1)) < nch;) {
+            std::vector<char>& b = buf[c];
+            b.resize(std::min<uint64_t>(CHUNK, n - c * CHUNK) * 64);
+            char* o = b.data();
+            auto dec = [&o](uint64_t v) {
+                char t[20];
+                int m = 0;
+                do t[m++] = (char)('0' + v % 10); while ((v /= 10) != 0);
+                while (m) *o++ = t[--m];
+            };
+            for (uint64_t k = c * CHUNK; k < std::min<uint64_t>(n, (c + 1) * CHUNK); k++) {
+                dec(k);
+                *o++ = ' ';
+                for (int sh = 60; sh >= 0; sh -= 4) *o++ = HEX[(d[k] >> sh) & 15];
+                *o++ = ' ';
+                dec(r[k]);
+                *o++ = ' ';
+                int sh = 28;
+                while (sh > 0 && ((e[k] >> sh) & 15) == 0) sh -= 4;
+                for (; sh >= 0; sh -= 4) *o++ = HEX[(e[k] >> sh) & 15];
+                *o++ = '\n';
+            }
+            b.resize((size_t)(o - b.data()));
+        }
+    };
+    const uint64_t nt = std::min<uint64_t>(nch, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    std::vector<std::thread> pool;
+    for (uint64_t i = 1; i < nt; i++) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+    bool ok = true;
+    for (auto& b : buf) ok = ok && fwrite(b.data(), 1, b.size(), f) == b.size();
+    return (fclose(f) == 0 && ok) ? DASH_OK : fail(h, DASH_EIO, "write %s", path);
 }
 
 int dash_simulate_dir(const char* dir, uint32_t num_procs, uint32_t cache_size, uint32_t max_instr,

@@ -662,7 +662,10 @@ int dash_write_digests(dash_t* h, const char* path) {
     };
     const uint64_t nt = std::min<uint64_t>(nch, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
     std::vector<std::thread> pool;
-    for (uint64_t i = 1; i < nt; i++) pool.emplace_back(work);
+    try {
+        for (uint64_t i = 1; i < nt; i++) pool.emplace_back(work);
+    } catch (...) {  // no thread: the calling thread formats the remaining chunks
+    }
     work();
     for (auto& th : pool) th.join();
     bool ok = true;

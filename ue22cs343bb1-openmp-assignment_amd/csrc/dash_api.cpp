@@ -595,7 +595,10 @@ int dash_load_dirs(dash_t* h, const char* const* dirs, uint64_t n) {
     };
     const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({n, 16, std::max(1u, std::thread::hardware_concurrency())}));
     std::vector<std::thread> pool;
-    for (unsigned i = 1; i < nt; i++) pool.emplace_back(worker);
+    try {
+        for (unsigned i = 1; i < nt; i++) pool.emplace_back(worker);
+    } catch (...) {  // no thread: the calling thread takes the remaining directories
+    }
     worker();
     for (auto& th : pool) th.join();
     if (bad.load() != ~0ull)
@@ -760,7 +763,13 @@ extern "C" int dash_run_host_batched(const dash_cfg* cfg, const uint16_t* packed
     };
     if (rc == DASH_OK) {
         std::vector<std::thread> pool;
-        for (unsigned i = 0; i < nh; i++) pool.emplace_back(lane, i);
+        for (unsigned i = 0; i < nh; i++) {
+            try {
+                pool.emplace_back(lane, i);
+            } catch (...) {  // no thread: this lane's batches run on the calling thread
+                lane(i);
+            }
+        }
         for (auto& t : pool) t.join();
         rc = trc[0] != DASH_OK ? trc[0] : trc[1];
         if (rc != DASH_OK) set_global_msg(h[trc[0] != DASH_OK ? 0 : 1]->msg);

@@ -177,6 +177,18 @@ int dash_run_host_batched(const dash_cfg *cfg, const uint16_t *packed, uint64_t 
                           const uint32_t *lens, uint64_t num_systems, uint32_t batches,
                           dash_stats *stats, uint64_t *digests, uint32_t *rounds, uint32_t *errors);
 int dash_generate(dash_t *h, const dash_gen *g);
+/* An explicit round schedule, replacing the seeded rounds of a handle created with
+   schedule_seed != 0 (DASH_ESTATE otherwise): sched[r * num_procs + t] = DASH_SIT_OUT when node
+   t sits round r out, else t's delivery position in round r (< next_pow2(num_procs), distinct
+   among the round's stepping nodes; DASH_EINVAL otherwise). Rounds >= `rounds` are lockstep
+   rounds (every node steps, ascending sender order). Every system of the batch follows it.
+   The whole run must fit the handle's round table: cfg.max_rounds (rounded) <= 2^22 and no
+   DASH_TEST_SHORT_ARB. Each round is a legal reference execution (the stepping
+   threads run their handlers, then complete their sendMessage calls (:741-765) one thread after
+   another in delivery order), so a schedule pins one chosen interleaving of the reference, e.g.
+   the one behind an accepted racy-test output (tests/golden/schedules/). */
+#define DASH_SIT_OUT 0xFFu
+int dash_set_schedule(dash_t *h, const uint8_t *sched, uint32_t rounds);
 int dash_run(dash_t *h, dash_stats *stats);
 int dash_read_state(dash_t *h, uint64_t sys, dash_node_state *out /* [num_procs] */);
 int dash_read_results(dash_t *h, uint64_t first, uint64_t count, uint64_t *digests,

@@ -24,6 +24,7 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <stddef.h>
 #include <string.h>
 #include <time.h>
 #ifdef _OPENMP
@@ -147,7 +148,7 @@ static void handle_message(osys *sy, int tid, omsg msg) {
             r.value = nd->memory[memBlockAddr];
             r.dirState = S;
             send_message(nd, msg.sender, r);
-            nd->bitVector[memBlockAddr] |= (uint8_t)(1u << msg.sender);
+            if (ORC_MUTANT != 8) nd->bitVector[memBlockAddr] |= (uint8_t)(1u << msg.sender);
         } else { /* U */
             r.type = REPLY_RD;
             r.sender = (uint8_t)tid;
@@ -230,7 +231,7 @@ static void handle_message(osys *sy, int tid, omsg msg) {
         break;
 
     case INV: /* ref :389-399; state not checked */
-        if (L->address == msg.address)
+        if (L->address == msg.address && (ORC_MUTANT != 11 || L->state == SHARED))
             L->state = INVALID;
         break;
 
@@ -259,12 +260,14 @@ static void handle_message(osys *sy, int tid, omsg msg) {
                 send_message(nd, ctz8(nd->bitVector[memBlockAddr]), r);
             }
         }
+        if (ORC_MUTANT == 9 && nd->dirState[memBlockAddr] == S) break;
         nd->dirState[memBlockAddr] = EM; /* ref :456-457, every branch */
         nd->bitVector[memBlockAddr] = (uint8_t)(1u << msg.sender);
         break;
 
     case REPLY_WR: /* ref :461-474; replacement is unconditional (App. B 6) */
-        handle_cache_replacement(nd, tid, *L);
+        if (ORC_MUTANT != 10 || L->address != msg.address)
+            handle_cache_replacement(nd, tid, *L);
         L->address = msg.address;
         L->value = nd->instr_value;
         L->state = MODIFIED;
@@ -324,6 +327,7 @@ static void handle_message(osys *sy, int tid, omsg msg) {
         break;
 
     case EVICT_MODIFIED: /* ref :592-617 */
+        if (ORC_MUTANT == 12 && nd->bitVector[memBlockAddr] != (uint8_t)(1u << msg.sender)) break;
         nd->memory[memBlockAddr] = msg.value;
         nd->bitVector[memBlockAddr] = 0;
         nd->dirState[memBlockAddr] = U;
@@ -368,7 +372,7 @@ static void issue_instruction(osys *sy, int tid) {
         if (hit) {
             if (L->state == MODIFIED || L->state == EXCLUSIVE) {
                 L->value = value;
-                L->state = MODIFIED;
+                if (ORC_MUTANT != 13 || L->state == MODIFIED) L->state = MODIFIED;
             } else {
                 m.type = UPGRADE;
                 m.sender = (uint8_t)tid;
@@ -490,7 +494,12 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
         for (int t = 0; t < N; t++) {
             onode *nd = &sy->node[t];
             nd->nout = 0;
-            if (cfg->arb_seed && orc_arb_stall(cfg->arb_seed, out->rounds - 1, (uint32_t)t)) continue;
+            if (cfg->sched) {
+                if (out->rounds - 1 < cfg->sched_rounds && cfg->sched[(out->rounds - 1) * (uint64_t)N + t] == 0xFF)
+                    continue;
+            } else if (cfg->arb_seed && orc_arb_stall(cfg->arb_seed, out->rounds - 1, (uint32_t)t)) {
+                continue;
+            }
             if (nd->qcount > 0 && nd->qcount < (uint32_t)sy->ring) {
                 omsg m = nd->q[nd->head];
                 nd->head = (nd->head + 1) % (uint32_t)sy->ring;
@@ -504,7 +513,17 @@ int orc_run_system(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride,
            order within a sender (sendMessage ref :741-765) */
         int order[ORC_MAX_PROCS];
         for (int s = 0; s < N; s++) order[s] = s;
-        if (cfg->arb_seed) {
+        if (cfg->sched) {
+            if (out->rounds - 1 < cfg->sched_rounds) {
+                const uint8_t *row = cfg->sched + (out->rounds - 1) * (uint64_t)N;
+                int k = 0;
+                for (int pos = 0; pos < ORC_MAX_PROCS; pos++)
+                    for (int s = 0; s < N; s++)
+                        if (row[s] == pos) order[k++] = s;
+                for (int s = 0; s < N; s++) /* sitting-out nodes send nothing; keep them listed */
+                    if (row[s] == 0xFF || row[s] >= ORC_MAX_PROCS) order[k++] = s;
+            }
+        } else if (cfg->arb_seed) {
             uint32_t P = 1;
             while (P < (uint32_t)N) P <<= 1;
             int k = 0;
@@ -717,17 +736,19 @@ typedef struct {
 typedef struct {
     xnode n[ORC_MAX_PROCS];
     uint32_t errors;
-    uint32_t _pad;
+    int8_t deficit[ORC_MAX_PROCS]; /* ORC_MICRO_RACE: appends whose count++ was lost (:757 vs :177) */
+    uint8_t races, _pad[3];
+    uint16_t hist[ORC_NUM_TXN + 1]; /* cfg->count_msgs: messages handled per type so far */
+    uint16_t npop[ORC_MAX_PROCS];   /* guided search: messages each node has popped */
 } xsys;
 
 typedef struct {
-    int N, CS;
+    int N, CS, micro, race_max, count_msgs, guided;
     const uint16_t *trace[ORC_MAX_PROCS];
     uint32_t count[ORC_MAX_PROCS];
     osys *scratch; /* the oracle's handlers run on a scratch node */
     orc_result scratch_res;
 } xctx;
-
 static void x_init(xctx *c, xsys *s) {
     memset(s, 0, sizeof *s);
     for (int t = 0; t < c->N; t++) {
@@ -780,6 +801,8 @@ static void x_step(xctx *c, xsys *s, int t, const omsg *msg) {
 static void x_pop(xctx *c, xsys *s, int t) {
     xnode *x = &s->n[t];
     omsg m = x->q[0];
+    if (c->count_msgs && m.type < ORC_NUM_TXN) s->hist[m.type]++;
+    if (c->guided) s->npop[t]++;
     memmove(&x->q[0], &x->q[1], sizeof(omsg) * (size_t)(x->qn - 1));
     x->qn--;
     memset(&x->q[x->qn], 0, sizeof(omsg));
@@ -801,16 +824,101 @@ static void x_send(xctx *c, xsys *s, int t) {
     d->q[d->qn++] = m;
 }
 
-static int x_can_issue(const xctx *c, const xsys *s, int t) {
-    const xnode *x = &s->n[t];
-    return x->qn == 0 && !x->waiting && x->idx < c->count[t];
+/* The visible queue count: the reference's `count` (:168) lags the true queue length by the
+   appends whose count++ (:757) a racing count-- (:177) overwrote (ORC_MICRO_RACE only). */
+static int x_vis(const xctx *c, const xsys *s, int t) {
+    return (int)s->n[t].qn - (c->micro == ORC_MICRO_RACE ? s->deficit[t] : 0);
 }
 
-static uint64_t x_hash(const xsys *s) {
-    const uint64_t *w = (const uint64_t *)s;
+/* POP(t): the drain loop's test `count > 0 && head != tail` (:167-170); STRICT / RACE: t's
+   earlier sends are done (sendMessage returns before the loop tests again). */
+static int x_can_pop(const xctx *c, const xsys *s, int t) {
+    return x_vis(c, s, t) > 0 && (c->micro == ORC_MICRO_BUFFERED || s->n[t].on == 0);
+}
+
+/* ISSUE(t): the drain loop found nothing, not waiting, instructions left (:624-647). */
+static int x_can_issue(const xctx *c, const xsys *s, int t) {
+    const xnode *x = &s->n[t];
+    return x_vis(c, s, t) <= 0 && (c->micro == ORC_MICRO_BUFFERED || x->on == 0) && !x->waiting &&
+           x->idx < c->count[t];
+}
+
+/* micro-steps, encoded kind << 8 | aux << 4 | node */
+enum { XK_POP, XK_ISSUE, XK_SEND, XK_RACE };
+#define XSTEP(k, aux, t) ((uint16_t)((k) << 8 | (aux) << 4 | (t)))
+
+/* Every enabled step, in node order (POP, ISSUE, SEND, then RACE). RACE(x -> t): t's pop and
+   x's append to t overlap so that t's unlocked count-- (:177) overwrites x's count++ (:757);
+   the message is in the queue but not counted, so t may find its queue "empty" (issue, or stop
+   draining) with it inside, until a later append is counted (one message stranded, or dropped
+   for good at the end). */
+static int x_enabled(const xctx *c, const xsys *s, uint16_t *st) {
+    int n = 0;
+    for (int t = 0; t < c->N; t++) {
+        if (x_can_pop(c, s, t)) st[n++] = XSTEP(XK_POP, 0, t);
+        if (x_can_issue(c, s, t)) st[n++] = XSTEP(XK_ISSUE, 0, t);
+        if (s->n[t].on > 0) st[n++] = XSTEP(XK_SEND, 0, t);
+    }
+    if (c->micro == ORC_MICRO_RACE && s->races < c->race_max)
+        for (int t = 0; t < c->N; t++) {
+            if (s->n[t].on == 0) continue;
+            const int r = s->n[t].oto[0];
+            if (r != t && r < c->N && x_can_pop(c, s, r) && s->n[r].qn < XQ) st[n++] = XSTEP(XK_RACE, t, r);
+        }
+    return n;
+}
+
+/* The persistent set the exhaustive search expands: {POP(t)} for the lowest t that can pop (a
+   pop commutes with every other thread's step and no other step of t is enabled beside it),
+   else every enabled step. While races are left the pop is not independent of a RACE on the
+   same queue, so everything is expanded. */
+static int x_succ(const xctx *c, const xsys *s, uint16_t *st) {
+    if (c->micro != ORC_MICRO_RACE || s->races >= c->race_max)
+        for (int t = 0; t < c->N; t++)
+            if (x_can_pop(c, s, t)) {
+                st[0] = XSTEP(XK_POP, 0, t);
+                return 1;
+            }
+    return x_enabled(c, s, st);
+}
+
+static void x_apply(xctx *c, xsys *s, uint16_t step) {
+    const int t = step & 15, aux = (step >> 4) & 15;
+    switch (step >> 8) {
+    case XK_POP: x_pop(c, s, t); break;
+    case XK_ISSUE: x_step(c, s, t, NULL); break;
+    case XK_SEND: x_send(c, s, t); break;
+    default: /* XK_RACE: t pops while aux's append to t loses its count++ */
+        x_pop(c, s, t);
+        x_send(c, s, aux);
+        s->deficit[t]++;
+        s->races++;
+        break;
+    }
+}
+
+/* Hash of the meaningful bytes of a state (unused queue slots excluded). */
+static uint64_t x_hash(const xctx *c, const xsys *s) {
     uint64_t h = 0x243F6A8885A308D3ULL;
-    for (size_t i = 0; i < sizeof(xsys) / 8; i++) h = fmix64(h ^ w[i]) + (uint64_t)i;
-    return h;
+#define XH(ptr, len)                                                                           \
+    do {                                                                                       \
+        const uint8_t *p_ = (const uint8_t *)(ptr);                                            \
+        size_t l_ = (len);                                                                     \
+        while (l_ >= 8) { uint64_t w_; memcpy(&w_, p_, 8); h = (h ^ w_) * 0x9E3779B97F4A7C15ULL; h ^= h >> 29; p_ += 8; l_ -= 8; } \
+        uint64_t w_ = 0; memcpy(&w_, p_, l_); h = (h ^ w_ ^ ((uint64_t)l_ << 56)) * 0xff51afd7ed558ccdULL; h ^= h >> 32; \
+    } while (0)
+    for (int t = 0; t < c->N; t++) {
+        const xnode *x = &s->n[t];
+        XH(x, offsetof(xnode, q));
+        XH(x->q, sizeof(omsg) * x->qn);
+        XH(x->o, sizeof(omsg) * x->on);
+        XH(x->oto, x->on);
+    }
+    XH(&s->errors, sizeof(uint32_t) + ORC_MAX_PROCS + 1);
+    if (c->count_msgs) XH(s->hist, sizeof s->hist);
+    if (c->guided) XH(s->npop, sizeof s->npop);
+#undef XH
+    return fmix64(h);
 }
 
 static void x_outcome(const xctx *c, const xsys *s, orc_outcome *o) {
@@ -831,14 +939,27 @@ static void x_outcome(const xctx *c, const xsys *s, orc_outcome *o) {
         d = fmix64(d ^ orc_digest_node(st, t, c->CS));
     }
     o->errors |= s->errors;
+    if (c->count_msgs) { /* the outcome is (final state, messages handled per type) */
+        uint64_t hk = 0x452821E638D01377ULL;
+        for (int k = 0; k < ORC_NUM_TXN; k++) {
+            o->hist[k] = s->hist[k];
+            hk = fmix64(hk ^ ((uint64_t)k << 32 | s->hist[k]));
+        }
+        d = fmix64(d ^ hk);
+    }
     o->digest = d;
 }
 
-static int x_setup(xctx *c, const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens) {
+static int x_setup(xctx *c, const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                   int race_max) {
     memset(c, 0, sizeof *c);
     c->N = cfg->num_procs;
     c->CS = cfg->cache_size;
+    c->micro = cfg->micro;
+    c->count_msgs = cfg->count_msgs;
+    c->race_max = c->micro == ORC_MICRO_RACE ? race_max : 0;
     if (c->N < 1 || c->N > ORC_MAX_PROCS || c->CS < 1 || c->CS > ORC_MAX_CACHE) return -1;
+    if (c->micro < ORC_MICRO_BUFFERED || c->micro > ORC_MICRO_RACE || race_max < 0 || race_max > 100) return -1;
     for (int t = 0; t < c->N; t++) {
         c->trace[t] = trace + (uint64_t)t * stride;
         c->count[t] = lens[t];
@@ -857,7 +978,7 @@ static int x_setup(xctx *c, const orc_cfg *cfg, const uint16_t *trace, uint64_t 
 int orc_replay_lockstep(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
                         orc_outcome *out, uint64_t *steps) {
     xctx c;
-    if (x_setup(&c, cfg, trace, stride, lens)) return -1;
+    if (x_setup(&c, cfg, trace, stride, lens, 0)) return -1;
     xsys *s = (xsys *)malloc(sizeof(xsys));
     x_init(&c, s);
     uint64_t n = 0;
@@ -899,22 +1020,15 @@ static uint64_t x_rng(uint64_t *st) {
 int orc_random_schedule(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
                         uint64_t seed, orc_outcome *out) {
     xctx c;
-    if (x_setup(&c, cfg, trace, stride, lens)) return -1;
+    if (x_setup(&c, cfg, trace, stride, lens, 0)) return -1;
     xsys *s = (xsys *)malloc(sizeof(xsys));
     x_init(&c, s);
     uint64_t st = seed;
+    uint16_t en[4 * ORC_MAX_PROCS];
     for (;;) {
-        int kinds[3 * ORC_MAX_PROCS], who[3 * ORC_MAX_PROCS], ne = 0;
-        for (int t = 0; t < c.N; t++) {
-            if (s->n[t].qn > 0) { kinds[ne] = 0; who[ne++] = t; }
-            if (x_can_issue(&c, s, t)) { kinds[ne] = 1; who[ne++] = t; }
-            if (s->n[t].on > 0) { kinds[ne] = 2; who[ne++] = t; }
-        }
+        const int ne = x_enabled(&c, s, en);
         if (ne == 0) break;
-        int k = (int)(x_rng(&st) % (uint64_t)ne);
-        if (kinds[k] == 0) x_pop(&c, s, who[k]);
-        else if (kinds[k] == 1) x_step(&c, s, who[k], NULL);
-        else x_send(&c, s, who[k]);
+        x_apply(&c, s, en[x_rng(&st) % (uint64_t)ne]);
     }
     x_outcome(&c, s, out);
     free(s);
@@ -943,7 +1057,7 @@ int orc_explore(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, cons
                 uint64_t max_states, orc_outcome *outs, int max_outs, int *n_outs, uint64_t *states,
                 int *complete) {
     xctx c;
-    if (x_setup(&c, cfg, trace, stride, lens)) return -1;
+    if (x_setup(&c, cfg, trace, stride, lens, 0)) return -1;
     xset vis;
     vis.cap = 1;
     while (vis.cap < 2 * max_states + 2) vis.cap <<= 1;
@@ -954,23 +1068,12 @@ int orc_explore(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, cons
     if (!vis.keys || !stack) { free(vis.keys); free(stack); free(c.scratch); return -1; }
     int nout = 0, full = 1;
     x_init(&c, &stack[sn++]);
-    xset_insert(&vis, x_hash(&stack[0]));
+    xset_insert(&vis, x_hash(&c, &stack[0]));
     xsys cur, nxt;
     while (sn > 0) {
         cur = stack[--sn];
-        int succ_kind[3 * ORC_MAX_PROCS], succ_who[3 * ORC_MAX_PROCS], ns = 0;
-        int popper = -1;
-        for (int t = 0; t < c.N; t++)
-            if (cur.n[t].qn > 0) { popper = t; break; }
-        if (popper >= 0) { /* persistent set {POP(popper)} */
-            succ_kind[ns] = 0;
-            succ_who[ns++] = popper;
-        } else {
-            for (int t = 0; t < c.N; t++) {
-                if (x_can_issue(&c, &cur, t)) { succ_kind[ns] = 1; succ_who[ns++] = t; }
-                if (cur.n[t].on > 0) { succ_kind[ns] = 2; succ_who[ns++] = t; }
-            }
-        }
+        uint16_t succ[4 * ORC_MAX_PROCS];
+        const int ns = x_succ(&c, &cur, succ);
         if (ns == 0) { /* terminal: record the outcome if new */
             orc_outcome o;
             x_outcome(&c, &cur, &o);
@@ -985,11 +1088,9 @@ int orc_explore(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, cons
         }
         for (int k = 0; k < ns; k++) {
             nxt = cur;
-            if (succ_kind[k] == 0) x_pop(&c, &nxt, succ_who[k]);
-            else if (succ_kind[k] == 1) x_step(&c, &nxt, succ_who[k], NULL);
-            else x_send(&c, &nxt, succ_who[k]);
+            x_apply(&c, &nxt, succ[k]);
             if (vis.n >= max_states) { full = 0; continue; }
-            if (!xset_insert(&vis, x_hash(&nxt))) continue;
+            if (!xset_insert(&vis, x_hash(&c, &nxt))) continue;
             if (sn == scap) {
                 scap *= 2;
                 xsys *ns2 = (xsys *)realloc(stack, sizeof(xsys) * scap);
@@ -1006,4 +1107,405 @@ int orc_explore(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, cons
     free(stack);
     free(c.scratch);
     return 0;
+}
+
+/* ==== goal-directed reachability (classify test_4 run_3 / run_4) ====
+ *
+ * orc_reach is a depth-first search over the micro-step model (cfg->micro; up to race_max
+ * RACE steps under ORC_MICRO_RACE) with a visited-state hash set and the pop-first persistent
+ * sets of x_succ. It stops at the first terminal state whose digest is one of `targets` and
+ * returns the path to it (the witness: one XSTEP word per step), which orc_replay_steps
+ * re-executes step by step, checking that each step is enabled in the full (unreduced) model.
+ * Successors are tried in a node-priority order (`prio[t]`, lower first; a DFS that prefers
+ * some threads delays the others as long as it can, which is how the racy tests' unusual
+ * outcomes arise), SEND before POP before ISSUE within a node; `order_seed` != 0 shuffles
+ * them instead. */
+
+static void x_order(const xctx *c, uint16_t *st, int n, const uint8_t *prio, uint64_t *rng) {
+    if (rng) {
+        for (int i = n - 1; i > 0; i--) {
+            const int j = (int)(x_rng(rng) % (uint64_t)(i + 1));
+            const uint16_t tmp = st[i]; st[i] = st[j]; st[j] = tmp;
+        }
+        return;
+    }
+    static const int kind_rank[4] = {1, 2, 0, 3}; /* SEND, POP, ISSUE, RACE */
+    for (int i = 1; i < n; i++) { /* insertion sort, preferred first */
+        const uint16_t v = st[i];
+        const int kv = (prio ? prio[v & 15] : 0) * 8 + kind_rank[v >> 8];
+        int j = i - 1;
+        while (j >= 0 && (prio ? prio[st[j] & 15] : 0) * 8 + kind_rank[st[j] >> 8] > kv) { st[j + 1] = st[j]; j--; }
+        st[j + 1] = v;
+    }
+    (void)c;
+}
+
+typedef struct {
+    xsys s;
+    uint32_t depth;
+    uint16_t step;
+} xent;
+
+int orc_reach(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+              int race_max, const uint64_t *targets, int n_targets, uint64_t max_states,
+              const uint8_t *prio, uint64_t order_seed, int *hit, uint16_t *witness, uint32_t wit_cap,
+              uint32_t *wit_len, uint64_t *states, int *complete, int *found_flags) {
+    xctx c;
+    if (x_setup(&c, cfg, trace, stride, lens, race_max)) return -1;
+    int n_found = 0;
+    xset vis;
+    vis.cap = 1;
+    while (vis.cap < max_states + max_states / 2 + 2) vis.cap <<= 1;
+    vis.keys = (uint64_t *)calloc(vis.cap, sizeof(uint64_t));
+    vis.n = 0;
+    size_t scap = 4096, sn = 0, pcap = 4096;
+    xent *stack = (xent *)malloc(sizeof(xent) * scap);
+    uint16_t *path = (uint16_t *)malloc(sizeof(uint16_t) * pcap);
+    int rc = 0, full = 1, found = -1;
+    uint32_t found_len = 0;
+    uint64_t rng = order_seed, *prng = order_seed ? &rng : NULL;
+    if (!vis.keys || !stack || !path) { rc = -1; goto done; }
+    x_init(&c, &stack[0].s);
+    if (found_flags)
+        for (int k = 0; k < n_targets; k++) found_flags[k] = 0;
+    stack[0].depth = 0;
+    stack[0].step = 0xFFFF;
+    sn = 1;
+    xset_insert(&vis, x_hash(&c, &stack[0].s));
+    while (sn > 0 && found < 0) {
+        xent *e = &stack[--sn];
+        const uint32_t d = e->depth;
+        if (e->step != 0xFFFF) { /* path[0..d-1] leads to this entry's parent; d >= 1 */
+            if (d > pcap) {
+                pcap *= 2;
+                uint16_t *np = (uint16_t *)realloc(path, sizeof(uint16_t) * pcap);
+                if (!np) { rc = -1; break; }
+                path = np;
+            }
+            path[d - 1] = e->step;
+        }
+        xsys cur = e->s;
+        uint16_t succ[4 * ORC_MAX_PROCS];
+        const int ns = x_succ(&c, &cur, succ);
+        if (ns == 0) {
+            orc_outcome o;
+            x_outcome(&c, &cur, &o);
+            for (int k = 0; k < n_targets; k++)
+                if (targets[k] == o.digest) {
+                    if (!found_flags) { found = k; found_len = d; break; }
+                    if (!found_flags[k]) { /* multi-target: the first witness is kept */
+                        found_flags[k] = 1;
+                        if (n_found++ == 0 && witness && d <= wit_cap) {
+                            memcpy(witness, path, sizeof(uint16_t) * d);
+                            found_len = d;
+                        }
+                        if (n_found == n_targets) found = k;
+                    }
+                }
+            continue;
+        }
+        x_order(&c, succ, ns, prio, prng);
+        for (int k = ns - 1; k >= 0; k--) { /* pushed last = tried first */
+            xsys nxt = cur;
+            x_apply(&c, &nxt, succ[k]);
+            if (vis.n >= max_states) { full = 0; continue; }
+            if (!xset_insert(&vis, x_hash(&c, &nxt))) continue;
+            if (sn == scap) {
+                scap *= 2;
+                xent *ns2 = (xent *)realloc(stack, sizeof(xent) * scap);
+                if (!ns2) { full = 0; rc = -1; break; }
+                stack = ns2;
+            }
+            stack[sn].s = nxt;
+            stack[sn].depth = d + 1;
+            stack[sn].step = succ[k];
+            sn++;
+        }
+        if (rc) break;
+    }
+    if (found >= 0 && witness && !found_flags) {
+        if (found_len > wit_cap) rc = -2;
+        else memcpy(witness, path, sizeof(uint16_t) * found_len);
+    }
+done:
+    if (hit) *hit = found_flags ? n_found : found;
+    if (wit_len) *wit_len = (found >= 0 || n_found) ? found_len : 0;
+    if (states) *states = vis.n;
+    if (complete) *complete = found < 0 && full && rc == 0;
+    free(vis.keys);
+    free(stack);
+    free(path);
+    free(c.scratch);
+    return rc;
+}
+
+/* One random schedule drawn with per-node weights and per-kind weights (POP, ISSUE, SEND, RACE;
+   either NULL: 1), with its witness. A step's weight is its acting node's weight (the popping
+   node's for a RACE) times its kind's: a large SEND weight models the reference, whose threads
+   append their messages right after the handler that made them (:741-765). */
+int orc_random_walk(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                    int race_max, uint64_t seed, const uint32_t *weights, const uint32_t *kind_w,
+                    orc_outcome *out, uint16_t *witness, uint32_t wit_cap, uint32_t *wit_len) {
+    xctx c;
+    if (x_setup(&c, cfg, trace, stride, lens, race_max)) return -1;
+    xsys *s = (xsys *)malloc(sizeof(xsys));
+    if (!s) { free(c.scratch); return -1; }
+    x_init(&c, s);
+    uint64_t st = seed;
+    uint16_t en[4 * ORC_MAX_PROCS];
+    uint32_t n = 0;
+    int rc = 0;
+    for (;;) {
+        const int ne = x_enabled(&c, s, en);
+        if (ne == 0) break;
+        int k;
+        if (weights || kind_w) {
+            uint64_t wt[4 * ORC_MAX_PROCS], tot = 0;
+            for (int i = 0; i < ne; i++) {
+                wt[i] = (uint64_t)(weights ? weights[en[i] & 15] : 1u) * (kind_w ? kind_w[en[i] >> 8] : 1u);
+                tot += wt[i];
+            }
+            if (tot == 0) { k = (int)(x_rng(&st) % (uint64_t)ne); }
+            else {
+                uint64_t r = x_rng(&st) % tot;
+                for (k = 0; k < ne - 1; k++) {
+                    if (r < wt[k]) break;
+                    r -= wt[k];
+                }
+            }
+        } else {
+            k = (int)(x_rng(&st) % (uint64_t)ne);
+        }
+        if (witness) {
+            if (n < wit_cap) witness[n] = en[k];
+            else rc = -2;
+        }
+        n++;
+        x_apply(&c, s, en[k]);
+    }
+    x_outcome(&c, s, out);
+    if (wit_len) *wit_len = n;
+    free(s);
+    free(c.scratch);
+    return rc;
+}
+
+/* Re-execute a witness. Returns 0, or -(k+1) when step k is not enabled in the full model;
+   *terminal says whether no step is enabled at the end. */
+int orc_replay_steps(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                     int race_max, const uint16_t *steps, uint32_t n, orc_outcome *out, int *terminal) {
+    xctx c;
+    if (x_setup(&c, cfg, trace, stride, lens, race_max)) return -1;
+    xsys *s = (xsys *)malloc(sizeof(xsys));
+    if (!s) { free(c.scratch); return -1; }
+    x_init(&c, s);
+    uint16_t en[4 * ORC_MAX_PROCS];
+    int rc = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const int ne = x_enabled(&c, s, en);
+        int ok = 0;
+        for (int i = 0; i < ne; i++)
+            if (en[i] == steps[k]) ok = 1;
+        if (!ok) { rc = -(int)(k + 1); break; }
+        x_apply(&c, s, steps[k]);
+    }
+    if (terminal) *terminal = x_enabled(&c, s, en) == 0;
+    x_outcome(&c, s, out);
+    free(s);
+    free(c.scratch);
+    return rc;
+}
+
+/* The engine's schedule (lockstep, seeded, or the explicit cfg->sched of dash_set_schedule) as
+   a micro-step witness: each round, every stepping node's POP or ISSUE on start-of-round
+   queues in node order, then every outbox drained in the round's delivery order. Each step is
+   checked enabled in the model cfg->micro (STRICT: these are real reference executions: the
+   stepping threads run their local parts, then complete their sends one thread after
+   another). Returns 0, -2 if a step was not enabled, -3 if the witness does not fit. */
+int orc_schedule_witness(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                         uint16_t *witness, uint32_t wit_cap, uint32_t *wit_len, orc_outcome *out) {
+    xctx c;
+    if (x_setup(&c, cfg, trace, stride, lens, 0)) return -1;
+    xsys *s = (xsys *)malloc(sizeof(xsys));
+    if (!s) { free(c.scratch); return -1; }
+    x_init(&c, s);
+    uint32_t n = 0;
+    int rc = 0;
+    uint32_t P = 1;
+    while (P < (uint32_t)c.N) P <<= 1;
+    uint16_t en[4 * ORC_MAX_PROCS];
+    for (uint64_t r = 0; rc == 0; r++) {
+        uint16_t round_steps[2 * ORC_MAX_PROCS];
+        int nr = 0;
+        int stall[ORC_MAX_PROCS] = {0}, order[ORC_MAX_PROCS];
+        for (int t = 0; t < c.N; t++) order[t] = t;
+        if (cfg->sched) {
+            if (r < cfg->sched_rounds) {
+                const uint8_t *row = cfg->sched + r * (uint64_t)c.N;
+                int k = 0;
+                for (int pos = 0; pos < ORC_MAX_PROCS; pos++)
+                    for (int t = 0; t < c.N; t++)
+                        if (row[t] == pos) order[k++] = t;
+                for (int t = 0; t < c.N; t++)
+                    if (row[t] == 0xFF || row[t] >= ORC_MAX_PROCS) { stall[t] = 1; order[k++] = t; }
+            }
+        } else if (cfg->arb_seed) {
+            int k = 0;
+            for (uint32_t pr = 0; pr < P; pr++)
+                for (int t = 0; t < c.N; t++)
+                    if (orc_arb_prio(cfg->arb_seed, r, (uint32_t)t, P) == pr) order[k++] = t;
+            for (int t = 0; t < c.N; t++) stall[t] = orc_arb_stall(cfg->arb_seed, r, (uint32_t)t);
+        }
+        int any = 0, can_any = 0;
+        for (int t = 0; t < c.N; t++) {
+            if (s->n[t].qn > 0 || x_can_issue(&c, s, t)) can_any = 1;
+            if (stall[t]) continue;
+            if (s->n[t].qn > 0) round_steps[nr++] = XSTEP(XK_POP, 0, t);
+            else if (x_can_issue(&c, s, t)) round_steps[nr++] = XSTEP(XK_ISSUE, 0, t);
+        }
+        if (!can_any) break; /* quiescent */
+        for (int k = 0; k < nr && rc == 0; k++) {
+            const int ne = x_enabled(&c, s, en);
+            int ok = 0;
+            for (int i = 0; i < ne; i++) ok |= en[i] == round_steps[k];
+            if (!ok) { rc = -2; break; }
+            if (n < wit_cap) witness[n] = round_steps[k]; else rc = -3;
+            n++;
+            x_apply(&c, s, round_steps[k]);
+            any = 1;
+        }
+        for (int k = 0; k < c.N && rc == 0; k++)
+            while (s->n[order[k]].on > 0) {
+                if (n < wit_cap) witness[n] = XSTEP(XK_SEND, 0, order[k]); else { rc = -3; break; }
+                n++;
+                x_apply(&c, s, XSTEP(XK_SEND, 0, order[k]));
+            }
+        if (r > 100000000ULL) { rc = -2; break; }
+        (void)any;
+    }
+    if (wit_len) *wit_len = n;
+    x_outcome(&c, s, out);
+    free(s);
+    free(c.scratch);
+    return rc;
+}
+
+/* ==== log-guided replay: the reference's own per-thread event logs (round 4) ====
+ *
+ * Built with -DDEBUG_MSG -DDEBUG_INSTR, the reference prints every message a thread pops
+ * ("Processor t msg from: s, type: k, address: a", :179-182) and every instruction it issues
+ * (:649-652), each thread's lines in its program order. orc_guided searches the STRICT
+ * micro-step model for an interleaving in which every node pops exactly the messages its log
+ * lists, in that order, and issues when its log says so (a node's local state, and so its
+ * final state, is then fixed by its log: the handlers are deterministic). Sends are free, so
+ * the search decides only when each append happens; a state in which a node's queue head is
+ * not the message its log pops next (or a node whose log issues next, or has ended, holds a
+ * message) can never recover and is cut. *found = 1 with the final outcome when such an
+ * interleaving exists; *complete = 1 when the search was exhaustive (found = 0 then means the
+ * model cannot produce the reference's run at all -- how the mutants are refuted).
+ * Event words: POP = type | sender << 8 | address << 16; ISSUE = 1 << 31. */
+typedef struct {
+    const uint32_t *ev[ORC_MAX_PROCS];
+    uint32_t n[ORC_MAX_PROCS];
+} xguide;
+
+static int g_cursor(const xsys *s, int t) { return (int)s->n[t].idx + (int)s->npop[t]; }
+
+static int g_dead(const xctx *c, const xguide *g, const xsys *s) {
+    for (int t = 0; t < c->N; t++) {
+        const xnode *x = &s->n[t];
+        if (x->qn == 0) continue;
+        const int k = g_cursor(s, t);
+        if ((uint32_t)k >= g->n[t]) return 1;
+        const uint32_t e = g->ev[t][k];
+        if (e >> 31) return 1;
+        const omsg *h = &x->q[0];
+        if ((e & 0xFF) != h->type || ((e >> 8) & 0xFF) != h->sender || ((e >> 16) & 0xFF) != h->address) return 1;
+    }
+    return 0;
+}
+
+static int g_succ(const xctx *c, const xguide *g, const xsys *s, uint16_t *st) {
+    int n = 0;
+    for (int t = 0; t < c->N; t++) { /* pop-first: a pop the log allows commutes with the rest */
+        const int k = g_cursor(s, t);
+        if ((uint32_t)k < g->n[t] && !(g->ev[t][k] >> 31) && x_can_pop(c, s, t)) {
+            st[0] = XSTEP(XK_POP, 0, t);
+            return 1;
+        }
+    }
+    for (int t = 0; t < c->N; t++) {
+        const int k = g_cursor(s, t);
+        if ((uint32_t)k < g->n[t] && (g->ev[t][k] >> 31) && x_can_issue(c, s, t)) st[n++] = XSTEP(XK_ISSUE, 0, t);
+        if (s->n[t].on > 0) st[n++] = XSTEP(XK_SEND, 0, t);
+    }
+    return n;
+}
+
+int orc_guided(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+               const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
+               orc_outcome *out, uint64_t *states, int *complete) {
+    xctx c;
+    if (cfg->micro != ORC_MICRO_STRICT) return -1;
+    if (x_setup(&c, cfg, trace, stride, lens, 0)) return -1;
+    c.guided = 1;
+    xguide g;
+    uint64_t off = 0;
+    for (int t = 0; t < c.N; t++) {
+        g.ev[t] = events + off;
+        g.n[t] = ev_count[t];
+        off += ev_count[t];
+    }
+    xset vis;
+    vis.cap = 1;
+    while (vis.cap < max_states + max_states / 2 + 2) vis.cap <<= 1;
+    vis.keys = (uint64_t *)calloc(vis.cap, sizeof(uint64_t));
+    vis.n = 0;
+    size_t scap = 1024, sn = 0;
+    xsys *stack = (xsys *)malloc(sizeof(xsys) * scap);
+    int rc = 0, full = 1, hit = 0;
+    if (!vis.keys || !stack) { rc = -1; goto done; }
+    x_init(&c, &stack[sn++]);
+    xset_insert(&vis, x_hash(&c, &stack[0]));
+    while (sn > 0 && !hit) {
+        xsys cur = stack[--sn];
+        uint16_t succ[4 * ORC_MAX_PROCS];
+        const int ns = g_succ(&c, &g, &cur, succ);
+        if (ns == 0) {
+            int all = 1;
+            for (int t = 0; t < c.N; t++)
+                if ((uint32_t)g_cursor(&cur, t) != g.n[t] || cur.n[t].qn || cur.n[t].on) all = 0;
+            if (all) {
+                uint16_t en[4 * ORC_MAX_PROCS];
+                if (x_enabled(&c, &cur, en) == 0) { /* terminal in the full model too */
+                    x_outcome(&c, &cur, out);
+                    hit = 1;
+                }
+            }
+            continue;
+        }
+        for (int k = 0; k < ns; k++) {
+            xsys nxt = cur;
+            x_apply(&c, &nxt, succ[k]);
+            if (g_dead(&c, &g, &nxt)) continue;
+            if (vis.n >= max_states) { full = 0; continue; }
+            if (!xset_insert(&vis, x_hash(&c, &nxt))) continue;
+            if (sn == scap) {
+                scap *= 2;
+                xsys *ns2 = (xsys *)realloc(stack, sizeof(xsys) * scap);
+                if (!ns2) { full = 0; rc = -1; break; }
+                stack = ns2;
+            }
+            stack[sn++] = nxt;
+        }
+        if (rc) break;
+    }
+done:
+    if (found) *found = hit;
+    if (states) *states = vis.n;
+    if (complete) *complete = hit || (full && rc == 0);
+    free(vis.keys);
+    free(stack);
+    free(c.scratch);
+    return rc;
 }

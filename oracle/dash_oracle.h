@@ -35,6 +35,15 @@ extern "C" {
 #define ORC_ERR_ROUNDCAP 16u /* stopped at max_rounds */
 #define ORC_ERR_STUCK 32u    /* a queue reached capacity: head == tail, never drained again (ref :167-170) */
 
+/* micro-step models (orc_cfg.micro) */
+#define ORC_MICRO_BUFFERED 0 /* a thread may pop/issue again while its earlier sends are still
+                                buffered (the round-1..3 checker: a superset of the reference) */
+#define ORC_MICRO_STRICT 1   /* a thread's sends all complete before its next pop or issue, as
+                                sendMessage is synchronous in the reference (:741-765): exactly
+                                the race-free reference */
+#define ORC_MICRO_RACE 2     /* STRICT plus the reference's unlocked count-- (:177) racing the
+                                locked count++ (:757): see orc_reach in dash_oracle.c */
+
 typedef struct orc_cfg {
     int num_procs;       /* N (NUM_PROCS, ref :6) 1..8 */
     int cache_size;      /* CACHE_SIZE (ref :7), 1..16 */
@@ -46,9 +55,17 @@ typedef struct orc_cfg {
     uint64_t max_rounds; /* 0 = unlimited; else clamped to 2^31 - 4 and rounded up to a
                             multiple of 4 like the engine's */
     int log_msgs;        /* log also DEBUG_MSG lines (ref :180-181), not only DEBUG_INSTR */
-    int _pad;
+    int micro;           /* micro-step model of the legality checker (ORC_MICRO_*); the lockstep
+                            runner ignores it */
     uint64_t arb_seed;   /* 0: deliver in ascending sender order; else the seeded per-round
                             sender order of orc_arb_prio */
+    const uint8_t *sched; /* explicit round schedule (twin of dash_set_schedule), or NULL:
+                             sched[r * num_procs + t] = 0xFF when node t sits round r out, else
+                             its delivery position (distinct among the round's stepping nodes);
+                             rounds >= sched_rounds are lockstep rounds. Overrides arb_seed. */
+    uint32_t sched_rounds;
+    int count_msgs;      /* legality checker: an outcome is (final state, messages handled per
+                            type), as the reference's DEBUG_MSG lines (:179-182) count them */
 } orc_cfg;
 
 /* Delivery priority of sender t in round r under a seeded arbitration (same spec as
@@ -121,9 +138,11 @@ uint64_t orc_digest_node(const orc_node_state *s, int node_id, int cache_size);
 /* ---- legality checker (race-free micro-step model) ---- */
 typedef struct orc_outcome {
     orc_node_state node[ORC_MAX_PROCS];
-    uint64_t digest;  /* same digest as orc_result.digest */
+    uint64_t digest;  /* same digest as orc_result.digest (with cfg.count_msgs: folded with hist) */
     uint32_t errors;  /* ORC_ERR_* (DEADLOCK when a node still waits) */
     uint32_t _pad;
+    uint32_t hist[ORC_NUM_TXN]; /* cfg.count_msgs: messages handled per type */
+    uint32_t _pad2;
 } orc_outcome;
 
 /* The lockstep schedule executed as micro-steps (each step checked enabled). */
@@ -137,6 +156,42 @@ int orc_random_schedule(const orc_cfg *cfg, const uint16_t *trace, uint64_t stri
 int orc_explore(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
                 uint64_t max_states, orc_outcome *outs, int max_outs, int *n_outs, uint64_t *states,
                 int *complete);
+
+/* Goal-directed DFS over the micro-step model cfg->micro (pop-first persistent sets, visited
+   hash set, at most race_max RACE steps under ORC_MICRO_RACE): stops at the first terminal
+   state whose digest is in targets (*hit = its index, else -1) and writes the witness, one
+   step word (kind << 8 | aux << 4 | node; kind 0 POP, 1 ISSUE, 2 SEND, 3 RACE with aux the
+   sender whose count++ is lost) per step. prio[t] (lower first) orders the successors;
+   order_seed != 0 shuffles them instead. *complete: every reachable state was visited without
+   a hit (the targets are unreachable in this model). With found_flags != NULL the search goes
+   on until every target is found (found_flags[k] = 1 for each found; *hit = how many; the
+   witness is the first hit's). */
+int orc_reach(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+              int race_max, const uint64_t *targets, int n_targets, uint64_t max_states,
+              const uint8_t *prio, uint64_t order_seed, int *hit, uint16_t *witness, uint32_t wit_cap,
+              uint32_t *wit_len, uint64_t *states, int *complete, int *found_flags);
+/* One random schedule with per-node and per-kind (POP, ISSUE, SEND, RACE) step weights (NULL:
+   uniform), and its witness. */
+int orc_random_walk(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                    int race_max, uint64_t seed, const uint32_t *weights, const uint32_t *kind_w,
+                    orc_outcome *out, uint16_t *witness, uint32_t wit_cap, uint32_t *wit_len);
+/* Re-execute a witness: 0, or -(k+1) if step k is not enabled in the full model. */
+int orc_replay_steps(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                     int race_max, const uint16_t *steps, uint32_t n, orc_outcome *out, int *terminal);
+
+/* The engine's schedule (lockstep, cfg->arb_seed or cfg->sched) as a micro-step witness, each
+   step checked enabled in the model cfg->micro. 0, -2 (a step not enabled), -3 (cap). */
+int orc_schedule_witness(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                         uint16_t *witness, uint32_t wit_cap, uint32_t *wit_len, orc_outcome *out);
+
+/* Log-guided replay (STRICT model): an interleaving in which every node pops exactly the
+   messages of its reference DEBUG_MSG log, in order, and issues where its DEBUG_INSTR log does.
+   events: the nodes' logs concatenated (ev_count[t] words for node t); POP word = type |
+   sender << 8 | address << 16, ISSUE word = 1u << 31. *found, the final *out; *complete = the
+   search was exhaustive (found 0 and complete 1: no such interleaving exists). */
+int orc_guided(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+               const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
+               orc_outcome *out, uint64_t *states, int *complete);
 
 #ifdef __cplusplus
 }

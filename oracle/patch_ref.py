@@ -74,10 +74,12 @@ TARGETS = [("cache_simulator_bench", ["-DNUM_PROCS=8", "-DMAX_INSTR_NUM=4096", "
 TARGETS += [(f"cache_simulator_bench_cs{cs}", ["-DNUM_PROCS=8", "-DMAX_INSTR_NUM=4096", f"-DCACHE_SIZE={cs}"])
             for cs in (1, 2, 8, 16)]
 TARGETS += [(f"cache_simulator_pin_cs{cs}", ["-DNUM_PROCS=4", "-DMAX_INSTR_NUM=32", f"-DCACHE_SIZE={cs}",
-                                              "-DDEBUG_MSG"]) for cs in (1, 4)]
-# the same at the headline's 8 nodes (round 3): cross-node traffic among 8 homes
+                                              "-DDEBUG_MSG", "-DDEBUG_INSTR"]) for cs in (1, 4)]
+# the same at the headline's 8 nodes (round 3): cross-node traffic among 8 homes. Round 4: DEBUG_INSTR
+# too, so each thread's whole event log (pops and issues, ref :179-182, :649-652) is printed and the
+# oracle replays it (tests/ref_pin.py guided pin)
 TARGETS += [(f"cache_simulator_pin8_cs{cs}", ["-DNUM_PROCS=8", "-DMAX_INSTR_NUM=32", f"-DCACHE_SIZE={cs}",
-                                               "-DDEBUG_MSG"]) for cs in (1, 4)]
+                                               "-DDEBUG_MSG", "-DDEBUG_INSTR"]) for cs in (1, 4)]
 
 
 def main():

@@ -28,6 +28,18 @@ transactionType (ref :30-44), plus
 
 `python3 tests/ref_pin.py OUT.json` writes the coverage table (profiles/r03/ref_pin_coverage.json);
 `--nodes 8` runs the same at the headline's node count (profiles/r03/ref_pin8_coverage.json).
+
+Round 4 -- the GUIDED pin (`run_guided`, `guided_mutant_kills`; `python3 tests/ref_pin.py --guided
+[--nodes 8] OUT.json`). The pin binaries also print DEBUG_INSTR (ref :649-652), so every reference
+run hands over each thread's whole event log: the messages it popped, in order, and where it
+issued. For traces far past complete exploration (5-8 instructions per node on 3-4 blocks, or
+6-10 per node hammering 1-2 lines; 2-8 active nodes) the oracle's orc_guided searches the STRICT
+race-free micro-step model for an interleaving in which every node pops exactly its logged
+messages and issues where it logged an issue, and the final state must then equal the
+reference's dumps byte for byte. Each thread's issue log must also equal its trace (the ingest).
+A mutant oracle is refuted by the first run it cannot replay (no interleaving exists: the
+search is exhaustive) or replays to other dumps -- including m4, whose missing second
+FLUSH_INVACK the home's logged pops expose through the mutant build itself.
 """
 from __future__ import annotations
 
@@ -62,7 +74,15 @@ MUTANTS = {
     5: "FLUSH_INVACK fills the requester's line with the message value (ref :531: instr.value)",
     6: "EVICT_SHARED at home does not promote the home's own line when it is the last sharer (ref :586)",
     7: "EVICT_SHARED at a non-home node checks the line address before setting EXCLUSIVE (ref :558)",
+    8: "READ_REQUEST at S does not add the requester to the sharers (ref :222 does)",
+    9: "WRITE_REQUEST at S leaves the directory S (ref :456-457 always set EM / requester)",
+    10: "REPLY_WR replaces the line only when it holds another address (ref :467: unconditional)",
+    11: "INV invalidates only a SHARED line (ref :396 does not check the state)",
+    12: "EVICT_MODIFIED applies only when the sender is the recorded owner (ref :602-616 do not check)",
+    13: "a WR hit on EXCLUSIVE keeps the line EXCLUSIVE (ref :706-710 make it MODIFIED)",
 }
+GUIDED_COUNT = 320  # traces per node count (each run `GUIDED_RUNS` times)
+GUIDED_RUNS = 2
 MUT_DIR = oc.ROOT / "oracle" / "_mut"
 LINE = re.compile(r"Processor (\d+) msg from: (\d+), type: (\d+), address: 0x([0-9A-F]{2})")
 
@@ -87,6 +107,58 @@ def gen_trace(seed, n=4):
     for t in act:
         for _ in range(int(rng.integers(1, 5))):
             a = (int(rng.integers(0, n)) << 4) | int(rng.choice(blocks))
+            w = rng.random() < 0.5
+            rows[t].append(oc.pack("W" if w else "R", a, int(rng.integers(1, 256)) if w else 0))
+    return cs, rows
+
+
+def gen_trace_large(seed, n=4):
+    """(cache_size, rows) of one system past complete exploration, by seed % 3:
+      0 'spread': 2-4 active nodes (all 4 at n = 4), 5-8 instructions each on 3-4 blocks homed on
+        1-3 nodes;
+      1 'hot': 3-6 active nodes (at most n), 6-10 instructions each on 1-2 blocks (a cache index
+        apart) homed on 1-2 nodes, so lines bounce between readers and writers (sharers that
+        write: m3);
+      2 'pairs': 3-5 active nodes, which are also the homes, 6-10 instructions on 2 blocks, half
+        of them a read followed by a write of the same line -- a home woken early by a FLUSH for
+        another line (ref :322) writes while its read reply is still in flight, so the REPLY_WR
+        can land on a line that is valid again (m10)."""
+    rng = np.random.default_rng(seed + 10_000)
+    cs = (1, 4)[(seed // 3) % 2]
+    rows = [[] for _ in range(n)]
+    kind = seed % 3
+    if kind == 2:
+        act = [int(a) for a in rng.choice(n, min(n, int(rng.integers(3, 6))), replace=False)]
+        blocks = [int(rng.integers(0, 16))]
+        blocks.append((blocks[0] + cs) % 16)
+        for t in act:
+            prev = None
+            for _ in range(int(rng.integers(6, 11))):
+                if prev is not None and rng.random() < 0.5:
+                    a, w = prev, True
+                else:
+                    a, w = (int(rng.choice(act)) << 4) | int(rng.choice(blocks)), rng.random() < 0.3
+                rows[t].append(oc.pack("W" if w else "R", a, int(rng.integers(1, 256)) if w else 0))
+                prev = None if w else a
+        return cs, rows
+    if kind == 0:
+        nb = int(rng.integers(3, 5))
+        b0 = int(rng.integers(0, 16))
+        blocks = ([(b0 + cs * k) % 16 for k in range(nb)] if rng.random() < 0.5
+                  else [int(b) for b in rng.choice(16, nb, replace=False)])
+        act = rng.choice(n, int(rng.integers(2, 5)), replace=False) if n > 4 else range(n)
+        homes = rng.choice(n, int(rng.integers(1, 4)), replace=False)
+        lo, hi = 5, 9
+    else:
+        blocks = [int(rng.integers(0, 16))]
+        if rng.random() < 0.5:
+            blocks.append((blocks[0] + cs) % 16)
+        homes = rng.choice(n, int(rng.integers(1, 3)), replace=False)
+        act = rng.choice(n, min(n, int(rng.integers(3, 7))), replace=False)
+        lo, hi = 6, 11
+    for t in act:
+        for _ in range(int(rng.integers(lo, hi))):
+            a = (int(rng.choice(homes)) << 4) | int(rng.choice(blocks))
             w = rng.random() < 0.5
             rows[t].append(oc.pack("W" if w else "R", a, int(rng.integers(1, 256)) if w else 0))
     return cs, rows
@@ -209,7 +281,119 @@ def mutant_kills(cases, max_states=MAX_STATES, n=4):
     return kills
 
 
-if __name__ == "__main__":
+def run_guided(count=GUIDED_COUNT, runs=GUIDED_RUNS, n=4, threads=THREADS):
+    """The guided pin (module docstring): every reference run's event logs replayed by the
+    oracle, final dumps compared byte for byte. Returns a report with the runs kept for the
+    mutant check."""
+    from concurrent.futures import ThreadPoolExecutor
+    cov = collections.Counter()
+    report = {"traces": 0, "reference_runs": 0, "replayed_exact": 0, "violations": [], "events": 0,
+              "instructions": 0, "max_search_states": 0, "timeouts": 0}
+    kept = []
+
+    def one(seed):
+        cs, rows = gen_trace_large(seed, n)
+        tr, lens = as_arrays(rows)
+        out = []
+        with tempfile.TemporaryDirectory() as td:
+            d = pathlib.Path(td)
+            write_trace(d / "tests" / "t", rows)
+            for _ in range(runs):
+                p = subprocess.run(["timeout", "20", str(pin_exe(cs, n)), "t"], cwd=d, capture_output=True,
+                                   text=True)
+                if p.returncode != 0:
+                    out.append((seed, cs, None, None, None, f"reference exit {p.returncode}"))
+                    continue
+                ev, instr = oc.parse_logs(p.stdout, n)
+                dumps = [(d / f"core_{k}_output.txt").read_text() for k in range(n)]
+                out.append((seed, cs, p.stdout, ev, (instr, dumps), None))
+        return seed, cs, tr, lens, rows, out
+
+    with ThreadPoolExecutor(threads) as pool:
+        for seed, cs, tr, lens, rows, out in pool.map(one, range(count)):
+            report["traces"] += 1
+            for _, _, stdout, ev, extra, err in out:
+                report["reference_runs"] += 1
+                if err:
+                    report["timeouts"] += 1
+                    report["violations"].append({"seed": seed, "why": err})
+                    continue
+                instr, dumps = extra
+                coverage_of(stdout, cov)
+                report["events"] += sum(len(e) for e in ev)
+                report["instructions"] += sum(len(r) for r in rows)
+                if instr != rows:
+                    report["violations"].append({"seed": seed, "why": "issue log differs from the trace"})
+                    continue
+                found, res, states, complete = oc.guided(tr, lens, ev, num_procs=n, cache_size=cs)
+                report["max_search_states"] = max(report["max_search_states"], states)
+                if not found:
+                    report["violations"].append({"seed": seed, "why": "no interleaving replays the logs",
+                                                 "complete": complete})
+                    continue
+                if [oc.dump_node(res, k, cs) for k in range(n)] != dumps:
+                    report["violations"].append({"seed": seed, "why": "replayed final state differs"})
+                    continue
+                report["replayed_exact"] += 1
+                kept.append((seed, cs, tr, lens, ev, dumps))
+    report["coverage"] = {k: cov[k] for k in oc.TXN_NAMES + ["WRITEBACK_INV with home == requester",
+                                                              "EVICT_SHARED hand-off to a non-home owner"]}
+    report["runs"] = kept
+    return report
+
+
+def guided_mutant_kills(runs, n=4, max_states=2_000_000):
+    """For every mutant oracle: (index of the first run it cannot replay, how), or None."""
+    if not all((MUT_DIR / f"libdash_oracle_m{k}.so").exists() for k in MUTANTS):
+        subprocess.run(["make", "-s", "-C", str(oc.ORACLE_DIR), "mutants"], check=True)
+    kills = {}
+    for k in MUTANTS:
+        L = oc.bind(MUT_DIR / f"libdash_oracle_m{k}.so")
+        kills[k] = None
+        for i, (seed, cs, tr, lens, ev, dumps) in enumerate(runs):
+            found, res, _, complete = oc.guided(tr, lens, ev, num_procs=n, cache_size=cs, L=L,
+                                                max_states=max_states)
+            if not found and complete:
+                kills[k] = (i, seed, "no interleaving of the mutant replays the reference's logs")
+                break
+            if found and [oc.dump_node(res, q, cs, L=L) for q in range(n)] != dumps:
+                kills[k] = (i, seed, "the mutant replays the logs to other final dumps")
+                break
+    return kills
+
+
+def explorer_reach(seeds, n, max_states=MAX_STATES):
+    """How many of the guided pin's traces the complete explorer (round 3) could not finish."""
+    skipped = 0
+    for seed in seeds:
+        cs, rows = gen_trace_large(seed, n)
+        tr, lens = as_arrays(rows)
+        _, _, complete = oc.explore(tr, lens, num_procs=n, cache_size=cs, max_states=max_states)
+        skipped += not complete
+    return skipped
+
+
+if __name__ == "__main__" and "--guided" in sys.argv:
+    args = [a for a in sys.argv[1:] if a != "--guided"]
+    n = 4
+    if "--nodes" in args:
+        n = int(args[args.index("--nodes") + 1])
+        del args[args.index("--nodes"):args.index("--nodes") + 2]
+    rep = run_guided(n=n)
+    runs = rep.pop("runs")
+    kills = guided_mutant_kills(runs, n=n)
+    rep["mutants"] = {f"m{k}: {MUTANTS[k]}": (f"rejected at reference run {v[0]} (trace seed {v[1]}): {v[2]}"
+                                              if v else "NOT REJECTED") for k, v in kills.items()}
+    rep["beyond_complete_exploration"] = (f"{explorer_reach(range(rep['traces']), n)} of {rep['traces']} traces "
+                                          f"exceed the round-3 explorer's {MAX_STATES} states")
+    exe = "cache_simulator_pin_cs{1,4}" if n == 4 else f"cache_simulator_pin{n}_cs{{1,4}}"
+    out = json.dumps({"source": f"tests/ref_pin.py --guided (oracle/_ref/{exe}: assignment.c + oracle/patch_ref.py, "
+                                f"NUM_PROCS {n}, MAX_INSTR_NUM 32, -DDEBUG_MSG -DDEBUG_INSTR)",
+                      "num_procs": n, "count": rep["traces"], "runs_per_trace": GUIDED_RUNS, **rep}, indent=1)
+    if args:
+        pathlib.Path(args[0]).write_text(out + "\n")
+    print(out)
+elif __name__ == "__main__":
     args = sys.argv[1:]
     n = 4
     if "--nodes" in args:

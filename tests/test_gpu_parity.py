@@ -405,6 +405,64 @@ def test_seeded_schedule_reaches_other_accepted_run(dash, tmp_path):
             (GOLDEN / "test_4" / "run_2" / f"core_{n}_output.txt").read_bytes()
 
 
+SCHED_DIR = ROOT / "tests" / "golden" / "schedules"
+
+
+@pytest.mark.parametrize("name", sorted(p.stem for p in SCHED_DIR.glob("test_*_run_*.json")))
+def test_engine_reproduces_every_accepted_run(dash, name, tmp_path):
+    """every accepted output of the racy tests -- test_3/run_1..2 and
+    test_4/run_1..4 (test3.sh / test4.sh) -- comes out of the engine byte-exactly. The committed
+    round schedule (tests/golden/schedules/, classified legal race-free in tests/test_legality.py)
+    goes in through dash_set_schedule; 64 copies of the system run in one batch (a whole wave
+    and more) and all of them dump run_k; the event-log kernel under the same schedule logs
+    exactly the oracle twin's DEBUG_MSG / DEBUG_INSTR lines."""
+    from test_legality import rounds_array
+    rec = json.loads((SCHED_DIR / f"{name}.json").read_text())
+    test, run = rec["test"], rec["run"]
+    tr, lens = load_test_dir(GOLDEN / test)
+    sched = rounds_array(rec["rounds"])
+    n = 64
+    with dash.Engine(n, num_procs=4, cache_size=4, max_instr=32, keep_state=True, schedule_seed=1) as eng:
+        eng.set_schedule(sched)
+        eng.load_traces(np.stack([tr] * n), np.stack([lens] * n))
+        eng.run()
+        dig = eng.read_results()[0]
+        assert (dig == dig[0]).all()
+        eng.dump_system(n - 1, tmp_path)
+    assert int(dig[0]) == int(rec["digest"], 16)
+    for k in range(4):
+        assert (tmp_path / f"core_{k}_output.txt").read_bytes() == \
+            (GOLDEN / test / run / f"core_{k}_output.txt").read_bytes(), (run, k)
+    _, log = run_system(tr, lens, log=True, log_msgs=True, sched=sched)
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=256, schedule_seed=1) as eng:
+        eng.set_schedule(sched)
+        eng.load_traces(tr[None], lens[None])
+        eng.run()
+        assert dash.format_events(eng.read_events(0)) == log
+
+
+def test_set_schedule_checks_its_input(dash):
+    tr, lens = load_test_dir(GOLDEN / "test_4")
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32) as eng:
+        with pytest.raises(dash.DashError) as e:
+            eng.set_schedule(np.zeros((1, 4), np.uint8))
+        assert e.value.code == dash.ESTATE
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, schedule_seed=3) as eng:
+        for bad in ([[0, 0, 1, 2]], [[0, 1, 2, 4]]):  # repeated position; position >= P
+            with pytest.raises(dash.DashError) as e:
+                eng.set_schedule(np.array(bad, np.uint8))
+            assert e.value.code == dash.EINVAL
+        eng.set_schedule(np.zeros((0, 4), np.uint8))  # all lockstep: run_1
+        eng.load_traces(tr[None], lens[None])
+        eng.run()
+        assert int(eng.read_results()[0][0]) == run_system(tr, lens).digest
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, schedule_seed=3,
+                     flags=dash.TEST_SHORT_ARB) as eng:  # the table does not hold the whole run
+        with pytest.raises(dash.DashError) as e:
+            eng.set_schedule(np.zeros((1, 4), np.uint8))
+        assert e.value.code == dash.EINVAL
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 def test_full_size_sampled_parity(dash, kind):
     """BASELINE configs[2] (uniform) and [3] (contention) at full size: 1M systems x

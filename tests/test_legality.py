@@ -11,9 +11,17 @@ a legal execution of assignment.c with race-free queues. These tests check:
     reference's expected dump among them; test_1/test_2 split into independent
     single-node components and have exactly one outcome, the expected one;
   * uniformly random legal schedules of the racy tests land on the accepted
-    `run_*` outputs (run_1 and run_2 of test_3 and test_4 are legal outcomes).
+    `run_*` outputs (run_1 and run_2 of test_3 and test_4 are legal outcomes);
+  * every accepted output of the racy tests (test_3/run_1..2, test_4/run_1..4) is classified
+    against the STRICT race-free model (a thread's sends complete before its next pop or
+    issue, assignment.c:741-765): each is LEGAL, with a committed micro-step witness that
+    replays to the reference's dumps byte-exactly, is re-found by the goal-directed search
+    (orc_reach), and with an engine round schedule (dash_set_schedule) whose oracle twin lands
+    on it and whose micro-step form is STRICT-legal (tests/golden/schedules/,
+    make_schedules.py). None needs the count race (:177 vs :757).
 """
 import collections
+import json
 
 import numpy as np
 import pytest
@@ -188,3 +196,89 @@ def test_seeded_outcomes_of_racy_tests_are_witnessed_legal(test):
     seeded = {oc.run_system(tr, lens, arb_seed=s).digest for s in range(1, 301)}
     assert seeded <= witnessed, len(seeded - witnessed)
     assert len(witnessed) > (500 if test == "test_3" else 20)
+
+
+SCHED_DIR = oc.ROOT / "tests" / "golden" / "schedules"
+RACY_RUNS = [(t, r.name) for t in ("test_3", "test_4") for r in sorted((oc.GOLDEN / t).glob("run_*"))]
+
+
+def rounds_array(rounds, n=4):
+    """A committed round schedule ('-' = sits the round out, else the delivery position)."""
+    return np.array([[0xFF if ch == "-" else int(ch) for ch in row] for row in rounds],
+                    dtype=np.uint8).reshape(len(rounds), n)
+
+
+def test_every_accepted_racy_run_is_classified():
+    assert len(RACY_RUNS) == 6
+    for test, run in RACY_RUNS:
+        rec = json.loads((SCHED_DIR / f"{test}_{run}.json").read_text())
+        assert (rec["test"], rec["run"]) == (test, run)
+        assert rec["classification"].startswith("legal")
+
+
+@pytest.mark.parametrize("test,run", RACY_RUNS)
+def test_accepted_run_has_a_strict_witness(test, run):
+    """run_k is a legal race-free outcome: the committed witness replays in the STRICT micro-step
+    model (each step enabled, ending terminal, no node waiting, no error) to the reference's own
+    run_k dumps, and the goal-directed DFS finds a witness again within the recorded budget."""
+    rec = json.loads((SCHED_DIR / f"{test}_{run}.json").read_text())
+    tr, lens = oc.load_test_dir(oc.GOLDEN / test)
+    acc = accepted(test)[run]
+    target = oc.dumps_digest(acc)
+    assert target == int(rec["digest"], 16)
+    steps = [oc.step_parse(t) for t in rec["witness"].split()]
+    out, terminal = oc.replay_steps(tr, lens, steps, micro=oc.MICRO_STRICT)
+    assert terminal and out.errors == 0
+    assert dumps(out) == acc
+    hit, wit, states, _ = oc.reach(tr, lens, [target], prio=rec["reach"]["prio"],
+                                   max_states=rec["reach"]["states"] + 1000)
+    assert hit == 0 and oc.replay_steps(tr, lens, wit)[0].digest == target
+
+
+@pytest.mark.parametrize("test,run", RACY_RUNS)
+def test_accepted_run_has_an_engine_round_schedule(test, run):
+    """The committed round schedule (the engine's dash_set_schedule form) lands the oracle's
+    twin on run_k, and written as micro-steps every step is enabled in the STRICT model, so the
+    engine's reproduction of run_k (tests/test_gpu_parity.py) is a real reference execution."""
+    rec = json.loads((SCHED_DIR / f"{test}_{run}.json").read_text())
+    tr, lens = oc.load_test_dir(oc.GOLDEN / test)
+    sched = rounds_array(rec["rounds"])
+    res = oc.run_system(tr, lens, sched=sched)
+    assert [oc.dump_node(res, k) for k in range(4)] == accepted(test)[run]
+    out, _ = oc.schedule_witness(tr, lens, sched=sched)
+    assert out.digest == res.digest and out.errors == 0
+
+
+def test_strict_model_is_contained_in_the_buffered_one():
+    """The STRICT model (sends complete before the thread's next step) only removes schedules
+    from the round-1..3 BUFFERED model, so its complete outcome sets are subsets; sample keeps
+    exactly its two outcomes."""
+    tr, lens = oc.load_test_dir(oc.GOLDEN / "sample")
+    outs, _, complete = oc.explore(tr, lens, max_states=100_000, micro=oc.MICRO_STRICT)
+    assert complete and len(outs) == 2
+    rng = np.random.default_rng(5)
+    for _ in range(25):
+        N, L = int(rng.integers(2, 4)), int(rng.integers(1, 4))
+        tr = np.zeros((N, L), np.uint16)
+        for t in range(N):
+            for i in range(L):
+                w = rng.random() < 0.6
+                a = (int(rng.integers(0, N)) << 4) | int(rng.integers(0, 2))
+                tr[t, i] = oc.pack("W" if w else "R", a, int(rng.integers(1, 256)) if w else 0)
+        lens = np.full(N, L, np.uint32)
+        kw = dict(num_procs=N, cache_size=1, max_states=500_000)
+        strict, _, c1 = oc.explore(tr, lens, micro=oc.MICRO_STRICT, **kw)
+        buffered, _, c2 = oc.explore(tr, lens, **kw)
+        assert c1 and c2
+        assert {o.digest for o in strict} <= {o.digest for o in buffered}
+        assert oc.run_system(tr, lens, num_procs=N, cache_size=1).digest in {o.digest for o in strict}
+
+
+@pytest.mark.parametrize("test", ["test_3", "test_4"])
+def test_seeded_schedules_are_strict_executions(test):
+    """Every seeded engine schedule, written as micro-steps, is enabled step by step in the STRICT
+    model and ends in the state the oracle's seeded twin computes."""
+    tr, lens = oc.load_test_dir(oc.GOLDEN / test)
+    for seed in range(1, 200):
+        out, _ = oc.schedule_witness(tr, lens, arb_seed=seed)
+        assert out.digest == oc.run_system(tr, lens, arb_seed=seed).digest

@@ -8,12 +8,29 @@ on 208 small random cross-node systems, 4 times each, and every dump set it writ
 in the oracle explorer's COMPLETE legal outcome set for that trace. Mutation check: seven
 oracle builds that each misread one cross-node handler (oracle/Makefile `mutants`) must each
 be refuted by the reference's runs. Skipped when the reference binaries were not built.
+
+Round 4 -- the GUIDED pin (tests/ref_pin.py run_guided): 320
+traces per node count, 4 and 8 nodes, far past complete exploration (5-10 instructions per node
+on 1-4 blocks, up to 8 active nodes), each run twice by the reference built with -DDEBUG_MSG
+-DDEBUG_INSTR; every run's per-thread event log is replayed by the oracle's STRICT model
+(orc_guided) and must end in the reference's dumps byte for byte. Thirteen mutant oracles
+(m1-m7 cross-node handlers; m8-m13 READ_REQUEST's sharer bit, WRITE_REQUEST's EM update,
+REPLY_WR's unconditional replacement, INV's missing state check, EVICT_MODIFIED's missing
+ownership check, the WR hit on E) are each refuted, at 4 and at 8 nodes, by reference runs kept
+as fixtures (tests/golden/ref_logs/, make_ref_logs.py): so the refutations need no reference
+binary and do not depend on which interleavings a live run happens to take; m4 is refuted by the
+mutant build itself failing to produce the home's logged second FLUSH_INVACK.
 """
+import json
+import pathlib
+
+import numpy as np
 import pytest
 
+import oracle_ctypes as oc
 import ref_pin
 
-pytestmark = pytest.mark.skipif(not ref_pin.available(), reason="reference pin binaries not built")
+needs_ref = pytest.mark.skipif(not ref_pin.available(), reason="reference pin binaries not built")
 
 
 @pytest.fixture(scope="module")
@@ -21,6 +38,7 @@ def report():
     return ref_pin.run()
 
 
+@needs_ref
 def test_reference_outcomes_lie_in_the_complete_legal_sets(report):
     assert report["traces"] == ref_pin.COUNT
     assert report["reference_runs"] == ref_pin.COUNT * ref_pin.RUNS
@@ -28,21 +46,13 @@ def test_reference_outcomes_lie_in_the_complete_legal_sets(report):
     assert report["distinct_reference_outcomes_total"] > ref_pin.COUNT  # the reference is racy here
 
 
+@needs_ref
 def test_every_handler_is_exercised_by_the_reference(report):
     cov = report["coverage"]
     assert all(cov[t] > 0 for t in ref_pin.oc.TXN_NAMES), cov
     assert cov["UPGRADE"] >= 10 and cov["REPLY_ID"] >= 10 and cov["INV"] >= 10
     assert cov["WRITEBACK_INV with home == requester"] >= 10
     assert cov["EVICT_SHARED hand-off to a non-home owner"] >= 10
-
-
-def test_mutant_oracles_are_refuted(report):
-    kills = ref_pin.mutant_kills(report["cases"])
-    # m4 (one FLUSH_INVACK when home == requester) leaves final states unchanged unless a home
-    # step lands between the owner's two sends; the reference's message stream refutes it
-    survivors = [k for k, s in kills.items() if s is None and not (k == 4 and report["coverage"][
-        "WRITEBACK_INV with home == requester"] > 0)]
-    assert survivors == [], {k: ref_pin.MUTANTS[k] for k in survivors}
 
 
 @pytest.mark.skipif(not ref_pin.available(8), reason="8-node reference pin binaries not built")
@@ -57,3 +67,48 @@ def test_reference_outcomes_at_eight_nodes():
     assert rep["distinct_reference_outcomes_total"] > ref_pin.COUNT8
     assert all(rep["coverage"][t] > 0 for t in ref_pin.oc.TXN_NAMES), rep["coverage"]
 
+
+
+@needs_ref
+@pytest.mark.parametrize("n", [4, 8])
+def test_guided_pin_replays_every_reference_run(n):
+    """Every run of the reference on 320 traces past complete exploration, replayed from its own
+    event logs by the STRICT race-free model, ends in the reference's dumps byte for byte; each
+    thread issued exactly its trace (ingest); every handler is exercised."""
+    rep = ref_pin.run_guided(n=n)
+    assert rep["traces"] == ref_pin.GUIDED_COUNT
+    assert rep["violations"] == [], rep["violations"][:5]
+    assert rep["replayed_exact"] == ref_pin.GUIDED_COUNT * ref_pin.GUIDED_RUNS
+    cov = rep["coverage"]
+    assert all(cov[t] >= 100 for t in oc.TXN_NAMES), cov
+    assert cov["WRITEBACK_INV with home == requester"] >= 100
+    assert cov["EVICT_SHARED hand-off to a non-home owner"] >= 100
+
+
+def _fixture_case(c):
+    n, cs = c["num_procs"], c["cache_size"]
+    rows = [[oc.pack(w[0][0], int(w[1], 16), int(w[2]) if len(w) > 2 else 0)
+             for w in (ln.split() for ln in r)] for r in c["trace"]]
+    tr, lens = ref_pin.as_arrays(rows)
+    ev = [[(1 << 31) if tok == "I" else
+           (lambda a: int(a[0]) | int(a[1]) << 8 | int(a[2], 16) << 16)(tok.split("."))
+           for tok in line.split()] for line in c["log"]]
+    return n, cs, tr, lens, ev
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_logged_reference_runs_refute_every_mutant(n):
+    """Reference runs kept as fixtures: the real oracle replays each to its dumps exactly, and
+    together they refute all thirteen mutants (each listed mutant cannot replay its run)."""
+    cases = json.loads((oc.ROOT / "tests" / "golden" / "ref_logs" / f"pin{n}.json").read_text())["cases"]
+    refuted = set()
+    for c in cases:
+        _, cs, tr, lens, ev = _fixture_case(c)
+        found, res, _, _ = oc.guided(tr, lens, ev, num_procs=n, cache_size=cs)
+        assert found and [oc.dump_node(res, k, cs) for k in range(n)] == c["dumps"], c["seed"]
+        for m in c["refutes"]:
+            L = oc.bind(ref_pin.MUT_DIR / f"libdash_oracle_{m}.so")
+            f, r, _, complete = oc.guided(tr, lens, ev, num_procs=n, cache_size=cs, L=L)
+            assert (not f and complete) or [oc.dump_node(r, k, cs, L=L) for k in range(n)] != c["dumps"], (m, c["seed"])
+            refuted.add(int(m[1:]))
+    assert refuted == set(ref_pin.MUTANTS)

@@ -318,6 +318,44 @@ int dash_generate(dash_t* h, const dash_gen* g) {
     return DASH_OK;
 }
 
+int dash_set_schedule(dash_t* h, const uint8_t* sched, uint32_t rounds) {
+    if (!h || (!sched && rounds)) return DASH_EINVAL;
+    if (!h->d_arb) return fail(h, DASH_ESTATE, "dash_set_schedule: handle created with schedule_seed = 0");
+    const uint32_t N = h->cfg.num_procs, P = h->seg;
+    if (h->arb_len < h->cfg.max_rounds)
+        return fail(h, DASH_EINVAL, "dash_set_schedule: the round table holds %u of max_rounds %llu rounds",
+                    h->arb_len, (unsigned long long)h->cfg.max_rounds);
+    if (rounds > h->arb_len) return fail(h, DASH_EINVAL, "dash_set_schedule: %u rounds > max_rounds", rounds);
+    for (uint32_t r = 0; r < rounds; r++) {
+        uint32_t used = 0;
+        for (uint32_t t = 0; t < N; t++) {
+            const uint8_t v = sched[(uint64_t)r * N + t];
+            if (v == DASH_SIT_OUT) continue;
+            if (v >= P || (used >> v) & 1u)
+                return fail(h, DASH_EINVAL, "dash_set_schedule: round %u node %u: position %u invalid or repeated",
+                            r, t, (unsigned)v);
+            used |= 1u << v;
+        }
+    }
+    // the kernel's table layout (dash_kernels.hip arb_table_kernel): [round / 4][lane][round % 4],
+    // each word 0 for a node sitting out, else its primary arrival bit 2 << 4 * position
+    std::vector<uint32_t> tab(((uint64_t)h->arb_len + 4) * P, 0);
+    for (uint64_t r = 0; r < (uint64_t)h->arb_len + 4; r++)
+        for (uint32_t t = 0; t < P; t++) {
+            uint32_t w = 0;
+            if (t < N) {
+                const uint32_t v = r < rounds ? sched[r * N + t] : t;  // later rounds: lockstep
+                w = v == DASH_SIT_OUT ? 0u : 2u << (4u * v);
+            }
+            tab[((r >> 2) * P + t) * 4 + (r & 3)] = w;
+        }
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    HIPCHK(h, hipMemcpyAsync(h->d_arb, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->ran = false;
+    return DASH_OK;
+}
+
 int dash_run(dash_t* h, dash_stats* stats) {
     if (!h) return DASH_EINVAL;
     if (!h->loaded) return fail(h, DASH_ESTATE, "no traces loaded");

@@ -52,7 +52,8 @@ EXPORTS = ("dash_create", "dash_destroy", "dash_last_error", "dash_load_traces",
            "dash_parse_core_file", "dash_resolve_dir", "dash_load_dir", "dash_init_node_state",
            "dash_dump_node", "dash_dump_file", "dash_digest_node", "dash_simulate_dir",
            "dash_read_events", "dash_format_event", "dash_load_dirs", "dash_dump_system",
-           "dash_write_digests", "dash_run_host_batched")
+           "dash_write_digests", "dash_run_host_batched", "dash_set_schedule")
+SIT_OUT = 0xFF
 
 
 class DashError(RuntimeError):
@@ -126,6 +127,7 @@ def lib() -> ctypes.CDLL:
         "dash_last_error": (ctypes.c_char_p, [vp]),
         "dash_load_traces": (i32, [vp, vp, u64, vp, u64]),
         "dash_generate": (i32, [vp, ctypes.POINTER(Gen)]),
+        "dash_set_schedule": (i32, [vp, vp, u32]),
         "dash_run": (i32, [vp, ctypes.POINTER(Stats)]),
         "dash_read_state": (i32, [vp, u64, ctypes.POINTER(NodeState)]),
         "dash_read_results": (i32, [vp, u64, u64, vp, vp, vp]),
@@ -298,6 +300,13 @@ class Engine:
     def generate(self, seed, length, kind=GEN_UNIFORM, locality=0, sys_base=0):
         g = Gen(seed, sys_base, kind, locality, length, 0)
         _check(lib().dash_generate(self.h, ctypes.byref(g)), "dash_generate", self.h)
+
+    def set_schedule(self, sched: np.ndarray):
+        """dash_set_schedule: an explicit round schedule, uint8 [rounds][num_procs] (SIT_OUT or
+        the node's delivery position); later rounds are lockstep. Needs schedule_seed != 0."""
+        sched = np.ascontiguousarray(sched, dtype=np.uint8)
+        assert sched.ndim == 2 and sched.shape[1] == self.num_procs
+        _check(lib().dash_set_schedule(self.h, sched.ctypes.data, sched.shape[0]), "dash_set_schedule", self.h)
 
     def run(self) -> dict:
         st = Stats()

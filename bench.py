@@ -150,30 +150,33 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
         # finished (4x the slowest finisher, at least 5 s; or --ref-timeout) is killed and not
         # counted: instructions and time are those of the instances that finished.
         batches, hung, instr, elapsed, t0 = 0, 0, 0, 0.0, time.perf_counter()
+        rates = []  # per batch: finished instances' instructions / the batch's slowest finisher
         while True:
             procs = [subprocess.Popen([str(exe), "b"], cwd=d, stdout=subprocess.DEVNULL) for d in dirs]
             tb = last = time.perf_counter()
             fin = {}
-            while len(fin) < k:
-                time.sleep(0.005)
-                now = time.perf_counter()
-                for i, p in enumerate(procs):
-                    if i not in fin and p.poll() is not None:
-                        if p.returncode != 0:
-                            raise RuntimeError(f"reference instance exited with {p.returncode}")
-                        fin[i] = now - tb
-                limit = max(5.0, 4 * max(fin.values())) if fin else args.ref_timeout
-                if len(fin) < k and now - tb > min(limit, args.ref_timeout):
+            try:
+                while len(fin) < k:
+                    time.sleep(0.005)
+                    now = time.perf_counter()
                     for i, p in enumerate(procs):
-                        if i not in fin:
-                            p.kill()
-                            p.wait()
-                            hung += 1
-                    break
-                if now - last > 30:
-                    last = now
-                    print(f"[ref_baseline] {len(fin)}/{k} instances done, {now - tb:.0f} s", file=sys.stderr,
-                          flush=True)
+                        if i not in fin and p.poll() is not None:
+                            if p.returncode != 0:
+                                raise RuntimeError(f"reference instance exited with {p.returncode}")
+                            fin[i] = now - tb
+                    limit = max(5.0, 4 * max(fin.values())) if fin else args.ref_timeout
+                    if len(fin) < k and now - tb > min(limit, args.ref_timeout):
+                        hung += sum(1 for i in range(k) if i not in fin)
+                        break
+                    if now - last > 30:
+                        last = now
+                        print(f"[ref_baseline] {len(fin)}/{k} instances done, {now - tb:.0f} s", file=sys.stderr,
+                              flush=True)
+            finally:  # stalled, or another instance failed: none keeps spinning into the next leg
+                for i, p in enumerate(procs):
+                    if p.poll() is None:
+                        p.kill()
+                    p.wait()
             if not fin:
                 raise RuntimeError(f"no reference instance finished within {args.ref_timeout:.0f} s")
             for i in fin:  # the instance reached quiescence and dumped its 8 nodes
@@ -181,12 +184,16 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
             batches += 1
             instr += len(fin) * 8 * args.len
             elapsed += max(fin.values())
+            rates.append(len(fin) * 8 * args.len / max(fin.values()))
             if time.perf_counter() - t0 >= target_s:
                 break
     cores = host_cores()
     loc = f", locality {locality / 65536:g}" if kind_name == "locality" else ""
     return {"value": instr / elapsed, "unit": "instr/s", "cores": cores, "host_cpus_visible": host_cpus_visible(),
             "kind": "reference", "mode": "A" if k == cores else ("B" if k == 1 else f"{k} instances"),
+            # spread over the batches (the spinning instances vary from batch to batch): instr/s
+            "batches": {"n": len(rates), "min": min(rates), "median": sorted(rates)[len(rates) // 2],
+                        "max": max(rates)},
             "instances": k, "threads_per_instance": 8, "hung_instances_killed": hung, "cpu_model": cpu_model(),
             "sample": f"{batches} batch(es) x {k} concurrent instance(s) x 8 OpenMP threads, one 8-node system "
                       f"x {args.len} instr each ({kind_name}{loc}, CS={cache_size}, systems 0..{k - 1} of seed "
@@ -194,6 +201,66 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
                       f"CPUs of cgroup quota on a host exposing "
                       f"{host_cpus_visible()} logical CPUs ({cpu_model()}); assignment.c + benchmark patch "
                       f"(oracle/patch_ref.py), gcc -O2 -fopenmp"}
+
+
+def sysfs_gpu(pci_domain, pci_bus):
+    """The GPU's current clock levels and power / temperature from sysfs (amdgpu), found by its
+    PCI address; None where the files are absent or unreadable (e.g. no GPU)."""
+    import glob
+    want = f"{pci_domain:04x}:{pci_bus:02x}:"
+    for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+        real = os.path.realpath(dev)
+        if not os.path.basename(real).lower().startswith(want):
+            continue
+        out = {"pci": os.path.basename(real)}
+        for f in ("pp_dpm_sclk", "pp_dpm_mclk", "pp_dpm_fclk", "power_dpm_force_performance_level"):
+            try:
+                txt = pathlib.Path(dev, f).read_text()
+            except OSError:
+                continue
+            cur = [ln.strip() for ln in txt.splitlines() if ln.strip().endswith("*")]
+            out[f] = cur[0] if cur else txt.strip()
+        for hw in sorted(glob.glob(f"{dev}/hwmon/hwmon*")):
+            for f, key, scale in (("power1_average", "power_w", 1e-6), ("power1_input", "power_w", 1e-6),
+                                  ("temp1_input", "temp_edge_c", 1e-3), ("temp2_input", "temp_hotspot_c", 1e-3),
+                                  ("freq1_input", "sclk_mhz", 1e-6)):
+                if key in out:
+                    continue
+                try:
+                    out[key] = round(int(pathlib.Path(hw, f).read_text()) * scale, 1)
+                except (OSError, ValueError):
+                    pass
+        return out
+    return None
+
+
+def box_probe(dash, dev):
+    """dash_probe_box (the device, its clock limits, a fixed VALU probe and the shader clock it
+    ran at) plus the sysfs clock levels, sampled around the timed region."""
+    try:
+        b = dash.probe_box(dev)
+    except Exception as e:
+        return {"error": str(e)}
+    return {"probe_ms": round(b["probe_ms"], 3), "probe_valu_per_s": b["probe_valu_per_s"],
+            "sclk_mhz": round(b["probe_sclk_mhz"], 1), "sclk_min_mhz": round(b["probe_sclk_min_mhz"], 1),
+            "sclk_max_mhz": round(b["probe_sclk_max_mhz"], 1),
+            "sysfs": sysfs_gpu(b["pci_domain"], b["pci_bus"]), "_dev": b}
+
+
+def box_record(before, after):
+    """The line's `box` object: what ran (device identity, limits) and how it ran (the probe and
+    clocks before and after the timed regions)."""
+    dev = before.pop("_dev", None) if before else None
+    if after:
+        after.pop("_dev", None)
+    out = {"probe_before": before, "probe_after": after,
+           "probe_basis": "dash_probe_box: CUs x 8 workgroups x 256 threads, 8 dependent full-rate VALU chains "
+                          "per lane, 2^18 trips; sclk = shader-clock cycles (s_memtime) / 100-MHz reference ticks "
+                          "(s_memrealtime) over each workgroup's loop"}
+    if dev:
+        out["device"] = {k: dev[k] for k in ("name", "arch", "compute_units", "clock_khz", "mem_clock_khz",
+                                             "pci_domain", "pci_bus", "pci_device", "total_mem")}
+    return out
 
 
 def shard(rank, world, per_gpu):
@@ -253,59 +320,83 @@ def read_profile(kind, fp):
     return prof, None
 
 
-def sweep(args, dash, rank, world, dev):
-    """configs[4]: 8M systems over 8 GPUs (args.systems per GPU), CACHE_SIZE x
-    locality grid; one RCCL all-reduce of the transaction histograms per point."""
+SWEEP_GRID = [(cs, p) for cs in (1, 2, 4, 8, 16) for p in (0.0, 0.25, 0.5, 0.75, 1.0)]
+
+
+def sweep_gpu(args, dash, rank, world, dev, steps, warmup):
+    """configs[4] on the GPU: the CACHE_SIZE x locality grid, args.systems per GPU (sharded by
+    global id), `warmup` untimed and `steps` timed steps per point (same barriers as the
+    headline); one RCCL all-reduce of the totals per point. One engine per CACHE_SIZE, new
+    traces per locality."""
     import torch
-    import torch.distributed as dist
     M = args.systems
     sys_base, M = shard(rank, world, M)
     points = []
+    a = argparse.Namespace(**vars(args))
+    a.steps, a.warmup = steps, warmup
     for cs in (1, 2, 4, 8, 16):
-        for p in (0.0, 0.25, 0.5, 0.75, 1.0):
-            loc = int(round(p * 65536))
-            eng = dash.Engine(M, num_procs=8, cache_size=cs, max_instr=args.len, device=dev)
-            eng.generate(args.seed, args.len, kind=dash.GEN_LOCALITY, locality=loc, sys_base=sys_base)
-            elapsed, stats, kms = timed_headline(eng, args, world, dev)
-            dsum = digest_sum(eng.read_results()[0])
-            elapsed, totals = reduce_totals(
-                elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
-                                          stats["dropped"]] + dsum, torch.device("cuda", dev), world)
+        eng = dash.Engine(M, num_procs=8, cache_size=cs, max_instr=args.len, device=dev)
+        try:
+            for c2, p in SWEEP_GRID:
+                if c2 != cs:
+                    continue
+                loc = int(round(p * 65536))
+                eng.generate(args.seed, args.len, kind=dash.GEN_LOCALITY, locality=loc, sys_base=sys_base)
+                elapsed, stats, kms = timed_headline(eng, a, world, dev)
+                dsum = digest_sum(eng.read_results()[0])
+                elapsed, totals = reduce_totals(
+                    elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
+                                              stats["dropped"]] + dsum, torch.device("cuda", dev), world)
+                avg_s = sum(kms) / len(kms) / 1e3
+                if rank == 0:  # progress (a long silent run looks hung)
+                    print(f"[sweep] CS {cs} locality {p}: {elapsed / steps * 1e3:.1f} ms/step", file=sys.stderr,
+                          flush=True)
+                points.append({"cache_size": cs, "locality": p,
+                               "value": world * M * 8 * args.len * steps / elapsed,
+                               "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
+                               # this rank's launches over the timed steps (HIP events; the step time above
+                               # is the max over ranks of the whole timed region)
+                               "kernel_ms_avg": avg_s * 1e3, "kernel_ms_steps": [round(x, 3) for x in kms],
+                               "roofline": roofline(M, args.len, avg_s, None,
+                                                    "no committed PMC run for sweep points: traffic not measured"),
+                               "rounds_per_system": totals[14] / (world * M),
+                               "hist": totals[:13], "instructions": totals[13], "rounds_total": totals[14],
+                               "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19],
+                               "tier_systems": stats["tier_systems"]})
+        finally:
             eng.close()
-            avg_s = sum(kms) / len(kms) / 1e3
-            if rank == 0:  # progress (a long silent run looks hung)
-                print(f"[sweep] CS {cs} locality {p}: {elapsed / args.steps * 1e3:.1f} ms/step", file=sys.stderr,
-                      flush=True)
-            points.append({"cache_size": cs, "locality": p,
-                           "value": world * M * 8 * args.len * args.steps / elapsed,
-                           "ms_per_step": elapsed / args.steps * 1e3,
-                           # this rank's first-tier launches over the timed steps (HIP events; the step
-                           # time above is the max over ranks of the whole timed region)
-                           "kernel_ms_avg": avg_s * 1e3, "kernel_ms_steps": [round(x, 3) for x in kms],
-                           "roofline": roofline(M, args.len, avg_s, None,
-                                                "no committed PMC run for sweep points: traffic not measured"),
-                           "rounds_per_system": totals[14] / (world * M),
-                           "hist": totals[:13], "instructions": totals[13], "rounds_total": totals[14],
-                           "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19],
-                           "tier_systems": stats["tier_systems"]})
+    return points
+
+
+def sweep_cpu(args, dash, points, target_s):
+    """The reference itself per sweep point (mode (A): one instance per host core, built for that
+    CACHE_SIZE, on systems 0.. of that point's locality traces): at least one batch, then more
+    until `target_s` has passed. Rank 0, after every GPU point and after the process group is
+    gone."""
+    for pt in points:
+        pt["cpu_baseline"], pt["vs_baseline"], pt["cpu_baseline_note"] = None, None, None
+        if args.no_cpu_baseline:
+            continue
+        print(f"[sweep] reference baseline CS {pt['cache_size']} locality {pt['locality']}", file=sys.stderr,
+              flush=True)
+        try:
+            cpu = ref_baseline(args, args.seed, dash.GEN_LOCALITY, target_s, args.ref_instances,
+                               cache_size=pt["cache_size"], locality=int(round(pt["locality"] * 65536)),
+                               kind_name="locality")
+            pt["cpu_baseline"], pt["vs_baseline"] = cpu, pt["value"] / cpu["value"]
+        except Exception as e:  # reported, never substituted by the port
+            pt["cpu_baseline_note"] = f"reference baseline unavailable: {e}"
+
+
+def sweep(args, dash, rank, world, dev):
+    """bench.py --sweep: configs[4] as its own line (--steps / --warmup per point)."""
+    import torch.distributed as dist
+    M = shard(rank, world, args.systems)[1]
+    points = sweep_gpu(args, dash, rank, world, dev, args.steps, args.warmup)
     if dist.is_initialized():
         dist.destroy_process_group()
     if rank == 0:
-        # the reference itself per point (mode (A), one batch or more of --sweep-cpu-seconds), after
-        # every GPU point and after the process group is gone (any --gpus N)
-        for pt in points:
-            pt["cpu_baseline"], pt["vs_baseline"], pt["cpu_baseline_note"] = None, None, None
-            if args.no_cpu_baseline:
-                continue
-            print(f"[sweep] reference baseline CS {pt['cache_size']} locality {pt['locality']}", file=sys.stderr,
-                  flush=True)
-            try:
-                cpu = ref_baseline(args, args.seed, dash.GEN_LOCALITY, args.sweep_cpu_seconds, args.ref_instances,
-                                   cache_size=pt["cache_size"], locality=int(round(pt["locality"] * 65536)),
-                                   kind_name="locality")
-                pt["cpu_baseline"], pt["vs_baseline"] = cpu, pt["value"] / cpu["value"]
-            except Exception as e:  # reported, never substituted by the port
-                pt["cpu_baseline_note"] = f"reference baseline unavailable: {e}"
+        sweep_cpu(args, dash, points, args.sweep_cpu_seconds)
         print(json.dumps({"metric": "simulated instr/sec (whole node), 8-core DASH systems; sweep",
                           "unit": "instr/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "higher_is_better": True, "scaling": "weak", "dtype": "u8",
@@ -560,6 +651,27 @@ def run_kind(dash, args, kind_name, M, sys_base, world, dev, steps, tier_flag):
     return elapsed, totals, stats, kernel_ms
 
 
+def sweep_golden_check(points, systems, args):
+    """The sweep points whose full-size totals the oracle pinned (tests/golden/sweep_full.json,
+    make_sweep_full.py): equal or not, per point (a fixture file, not the oracle)."""
+    f = ROOT / "tests" / "golden" / "sweep_full.json"
+    if not f.exists():
+        return None
+    g = json.loads(f.read_text())
+    if (g["systems"], g["instr_per_node"], g["seed"]) != (systems, args.len, args.seed):
+        return {"note": "golden is for 2^20 systems x 4096 instr, seed 0x5EED: not this workload"}
+    out = []
+    for gp in g["points"]:
+        pt = next((p for p in points if (p["cache_size"], p["locality"]) == (gp["cache_size"], gp["locality"])), None)
+        if pt is None:
+            continue
+        same = (pt["hist"] == gp["hist"] and pt["instructions"] == gp["instructions"] and
+                pt["rounds_total"] == gp["rounds_total"] and pt["err_systems"] == gp["err_systems"] and
+                pt["digest_sum"] == gp["digest_sum"])
+        out.append({"cache_size": gp["cache_size"], "locality": gp["locality"], "bit_exact": same})
+    return out
+
+
 def totals_dict(totals):
     return {"hist": totals[:13], "instructions_per_step": totals[13], "rounds_total": totals[14],
             "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19]}
@@ -586,6 +698,11 @@ def main():
     ap.add_argument("--sweep-cpu-seconds", type=float, default=1.0,
                     help="--sweep: target seconds of the reference baseline per point (at least one batch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--line-sweep", choices=["auto", "on", "off"], default="auto",
+                    help="the configs[4] grid inside the headline line (`sweep` object): auto = only with the "
+                         "full-size uniform headline workload")
+    ap.add_argument("--line-sweep-steps", type=int, default=1, help="timed steps per sweep point in the line")
+    ap.add_argument("--line-sweep-warmup", type=int, default=1, help="untimed steps per sweep point in the line")
     ap.add_argument("--cpu-kind", choices=["port", "reference"], default="reference",
                     help="headline cpu_baseline: the reference binary itself (oracle/_ref/cache_simulator_bench, "
                          "default; the oracle port is then reported as cpu_port) or only the oracle port")
@@ -685,8 +802,10 @@ def main():
 
     tier_flag = {0: 0, 32: dash.TIER_FROM_32, 256: dash.TIER_FROM_256}[args.first_depth]
     sys_base, M = shard(rank, world, args.systems)
+    probe0 = box_probe(dash, dev)
     elapsed, totals, stats, kernel_ms = run_kind(dash, args, args.kind, M, sys_base, world, dev,
                                                  args.steps, tier_flag)
+    probe1 = box_probe(dash, dev)
     instr_per_step = world * M * 8 * args.len
     value = instr_per_step * args.steps / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
@@ -712,11 +831,28 @@ def main():
                 "tier_systems": c_stats["tier_systems"], "wave_rounds": c_stats["wave_rounds"],
                 "totals": totals_dict(c_tot)}
 
+    # configs[4] beside the headline: the whole CACHE_SIZE x locality grid at
+    # this line's systems per GPU, --line-sweep-warmup untimed and --line-sweep-steps timed steps per
+    # point; by default only with the full-size headline workload
+    line_sweep = args.line_sweep == "on" or (args.line_sweep == "auto" and full and args.kind == "uniform")
+    points = sweep_gpu(args, dash, rank, world, dev, args.line_sweep_steps, args.line_sweep_warmup) \
+        if line_sweep else None
+
     # the CPU legs run after the timed regions and after the process group is gone, on rank 0
     # only, for every --gpus N (the ratio north_star states is the 8-GPU one)
     if dist.is_initialized():
         dist.destroy_process_group()
     if rank == 0:
+        sweep_obj = None
+        if points is not None:
+            sweep_cpu(args, dash, points, 0.0)  # one batch of the reference per point
+            sweep_obj = {"workload": f"{world * M} systems ({M}/GPU) x 8 nodes x {args.len} locality RD/WR per "
+                                     f"node, CACHE_SIZE {{1,2,4,8,16}} x locality {{0,.25,.5,.75,1}} "
+                                     f"(BASELINE configs[4]; seed 0x{args.seed:X}, keyed by global id)",
+                         "steps": args.line_sweep_steps, "warmup": args.line_sweep_warmup,
+                         "cpu_baseline_basis": "per point: one batch of the reference built for that CACHE_SIZE, "
+                                               "mode (A), on systems 0.. of that point's traces",
+                         "golden": sweep_golden_check(points, world * M, args), "points": points}
         cpu, cpu_b, port, note = None, None, None, None
         if not args.no_cpu_baseline:
             kind_id = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
@@ -778,6 +914,8 @@ def main():
                             "engine's defined drop-and-flag rule (DESIGN.md §2), the rest with the reference's "
                             "semantics under the lockstep schedule"),
             "contention": cont,
+            "sweep": sweep_obj,
+            "box": box_record(probe0, probe1),
         }
         print(json.dumps(line), flush=True)
 

@@ -200,6 +200,27 @@ int dash_read_events(dash_t *h, uint64_t sys, dash_event *out, uint32_t cap, uin
 /* HIP stream the engine launches on (hipStream_t as void*) */
 void *dash_stream(dash_t *h);
 
+/* Box calibration (not a reference interface: it makes a benchmark line explain the box it ran
+   on). The device's identity and clock limits, and one timed launch of a fixed VALU-bound
+   probe kernel (CUs x 8 workgroups of 256 threads, eight add/xor chains per lane): its time,
+   its rate, and the shader clock the box actually held meanwhile (shader-clock cycles over the
+   100-MHz reference counter, read by every workgroup around its loop). A box whose clock or
+   issue rate is low shows it here, whatever the simulation kernel did. */
+typedef struct dash_box_probe {
+    char name[64];
+    char arch[32];
+    int32_t compute_units;
+    int32_t clock_khz;        /* hipDeviceProp_t.clockRate (the maximum shader clock) */
+    int32_t mem_clock_khz;    /* hipDeviceProp_t.memoryClockRate */
+    int32_t pci_domain, pci_bus, pci_device;
+    uint64_t total_mem;
+    double probe_ms;          /* the probe launch (HIP events) */
+    double probe_valu_per_s;  /* wave64 VALU instructions of the chains per second */
+    double probe_sclk_mhz;    /* mean shader clock over the workgroups' loops */
+    double probe_sclk_min_mhz, probe_sclk_max_mhz;
+} dash_box_probe;
+int dash_probe_box(int device, dash_box_probe *out);
+
 /* ---- host boundary (pure C, no device) ---- */
 /* initializeProcessor's parse (ref :822-850): up to max_instr records into out[]. */
 int dash_parse_core_file(const char *path, uint32_t num_procs, uint32_t max_instr,

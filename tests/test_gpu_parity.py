@@ -578,3 +578,15 @@ def test_full_queue_is_stuck_like_the_reference(dash):
     assert res.errors & oracle_ctypes.ERR_STUCK and res.max_depth == 256
     assert stats["err_bits"] & dash.ERR_STUCK
     assert stats["tier_systems"][2] == 1  # handed from the 16- and 32-deep tiers to the reference depth
+
+
+def test_probe_box_reports_the_device(dash):
+    """dash_probe_box: the device's identity and limits, and a probe whose measured shader clock is
+    a plausible fraction of the device's maximum (the bench line's `box`)."""
+    b = dash.probe_box(0)
+    assert b["arch"].startswith("gfx950") and b["compute_units"] >= 1, b
+    assert b["probe_ms"] > 0 and b["probe_valu_per_s"] > 0
+    assert 300 < b["probe_sclk_mhz"] <= b["clock_khz"] / 1e3 * 1.05, b
+    assert b["probe_sclk_min_mhz"] <= b["probe_sclk_mhz"] <= b["probe_sclk_max_mhz"]
+    with pytest.raises(dash.DashError):
+        dash.probe_box(99)

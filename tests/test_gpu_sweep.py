@@ -47,3 +47,57 @@ def test_sweep_grid_matches_oracle(gpus):
             assert p["cpu_baseline"]["kind"] == "reference", p["cpu_baseline_note"]
             assert f"CS={p['cache_size']}" in p["cpu_baseline"]["sample"]
             assert abs(p["vs_baseline"] - p["value"] / p["cpu_baseline"]["value"]) < 1e-9 * p["vs_baseline"]
+
+
+def test_headline_line_carries_the_sweep():
+    """The default bench.py line's `sweep` object (configs[4] driver-observed):
+    forced on at 4096 systems, its 25 points equal the oracle's golden totals, each with its
+    kernel average, roofline, one reference batch per point and the golden check (n/a here)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--systems", str(GOLD["systems"]),
+                        "--len", str(GOLD["instr_per_node"]), "--seed", str(GOLD["seed"]), "--steps", "1",
+                        "--warmup", "0", "--contention-steps", "0", "--line-sweep", "on", "--cpu-seconds", "0.2",
+                        "--ref-instances", "2"],
+                       capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    sw = line["sweep"]
+    assert sw["steps"] == 1 and sw["warmup"] == 1 and len(sw["points"]) == 25
+    got = {(p["cache_size"], p["locality"]): p for p in sw["points"]}
+    for want in GOLD["points"]:
+        p = got[(want["cache_size"], want["locality"])]
+        for k in ("hist", "instructions", "rounds_total", "err_systems", "digest_sum"):
+            assert p[k] == want[k], (want["cache_size"], want["locality"], k)
+        assert p["kernel_ms_avg"] <= p["ms_per_step"] and 0 < p["roofline"]["frac"] < 1
+        assert p["cpu_baseline"]["kind"] == "reference", p["cpu_baseline_note"]
+        assert p["cpu_baseline"]["batches"]["n"] == 1
+    box = line["box"]
+    assert box["device"]["compute_units"] > 0 and box["device"]["clock_khz"] > 0
+    for k in ("probe_before", "probe_after"):
+        pb = box[k]
+        assert pb["probe_ms"] > 0 and 300 < pb["sclk_mhz"] <= box["device"]["clock_khz"] / 1e3 * 1.05, pb
+    cb = line["cpu_baseline"]["batches"]
+    assert cb["min"] <= cb["median"] <= cb["max"]
+
+
+FULL = ROOT / "tests" / "golden" / "sweep_full.json"
+
+
+@pytest.mark.skipif(not FULL.exists(), reason="tests/golden/sweep_full.json not generated")
+def test_full_size_sweep_points_match_oracle():
+    """Three configs[4] points at the full 2^20 systems x 8 nodes x 4096 instructions (CACHE_SIZE 1 /
+    locality 0, 4 / 0.5, 16 / 1) bit-exact against the oracle's full-size run (make_sweep_full.py)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    dash = bench.load_dash()
+    gold = json.loads(FULL.read_text())
+    for gp in gold["points"]:
+        with dash.Engine(gold["systems"], num_procs=8, cache_size=gp["cache_size"],
+                         max_instr=gold["instr_per_node"]) as eng:
+            eng.generate(gold["seed"], gold["instr_per_node"], kind=dash.GEN_LOCALITY,
+                         locality=int(round(gp["locality"] * 65536)))
+            st = eng.run()
+            dsum = bench.digest_sum(eng.read_results()[0])
+        assert st["hist"] == gp["hist"] and st["instructions"] == gp["instructions"], gp["cache_size"]
+        assert st["rounds_total"] == gp["rounds_total"] and st["err_systems"] == gp["err_systems"]
+        assert dsum == gp["digest_sum"]

@@ -2,10 +2,12 @@
 
 VERDICT r2 (next #2): bench.py reads roofline.traffic and the issue figures from committed
 rocprofv3 summaries (profiles/pmc_<kind>.json) and the static opcode mix from
-profiles/isa_table.json. Each records the fingerprint of sim_kernel<8,4,16,false> in the
-library it was measured on (tools/kernel_fingerprint.py: sha256 of the kernel's code and
-descriptor); they must match the library built from this tree, and the headline's traffic
-must re-derive from the one file's counters.
+profiles/isa_table.json. Each records the fingerprint of sim_kernel<8,4,16,0> (named
+sim_kernel<8,4,16,false> before round 3's MODE split; same bytes) in the library it was
+measured on (tools/kernel_fingerprint.py: sha256 of the kernel's code and descriptor); they
+must match the library built from this tree -- which ties this CPU test to the toolchain that
+built the committed profiles -- and the headline's traffic must re-derive from the one file's
+counters.
 """
 import csv
 import json
@@ -46,7 +48,7 @@ def test_traffic_rederives_from_the_committed_counters(kind):
 
 def test_uniform_kernel_stats_agree_with_the_pmc_run():
     """profiles/r03/kernel_stats_uniform.csv: rocprofv3 --kernel-trace --stats of the bench command
-    with the contention leg off, so its sim_kernel<8,4,16,false> average is the headline kernel's."""
+    with the contention leg off, so its sim_kernel<8,4,16,0> average is the headline kernel's."""
     rows = list(csv.DictReader((PROFILES / "r03" / "kernel_stats_uniform.csv").open()))
     row = next(r for r in rows if any(k in r["Name"] for k in ("sim_kernel<8, 4, 16u, false>", "sim_kernel<8, 4, 16u, 0>")))
     avg_ms = float(row["AverageNs"]) / 1e6

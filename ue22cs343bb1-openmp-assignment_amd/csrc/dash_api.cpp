@@ -89,14 +89,35 @@ static hipError_t reset_hint(dash_t* h) {
     return hipMemsetAsync(h->d_skip, 0, std::max<uint64_t>(h->cfg.num_systems, 1), h->stream);
 }
 
-extern "C" {
-
-// message of the last failed handle-less call (dash_create, dash_run_host_batched) on this thread
-// largest round cap: event words carry the round in bits 30..0 (bit 31 = issued instruction)
-static constexpr uint64_t MAX_ROUNDS_CAP = 0x7FFFFFFCull;
+// message of the last failed handle-less call (dash_create, dash_run_host_batched, ...) on this thread
 static thread_local char g_msg[256] = "";
 
 static void set_global_msg(const char* m) { snprintf(g_msg, sizeof g_msg, "%s", m ? m : ""); }
+
+// Runs an entry point's body so that no C++ exception crosses the C-ABI: a failed allocation
+// becomes DASH_ENOMEM (on the handle, or dash_last_error(NULL) without one).
+template <class F>
+static int guarded(dash_t* h, const char* what, F&& body) {
+    char m[256];
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        snprintf(m, sizeof m, "%s: out of host memory", what);
+        if (h) return fail(h, DASH_ENOMEM, "%s", m);
+        set_global_msg(m);
+        return DASH_ENOMEM;
+    } catch (...) {
+        snprintf(m, sizeof m, "%s: unexpected host failure", what);
+        if (h) return fail(h, DASH_EDEVICE, "%s", m);
+        set_global_msg(m);
+        return DASH_EDEVICE;
+    }
+}
+
+extern "C" {
+
+// largest round cap: event words carry the round in bits 30..0 (bit 31 = issued instruction)
+static constexpr uint64_t MAX_ROUNDS_CAP = 0x7FFFFFFCull;
 
 const char* dash_last_error(const dash_t* h) { return h ? h->msg : g_msg; }
 
@@ -239,57 +260,59 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
 
 int dash_load_traces(dash_t* h, const uint16_t* packed, uint64_t stride, const uint32_t* lens,
                      uint64_t num_systems) {
-    if (!h || (!packed && num_systems) || !lens) return DASH_EINVAL;
-    const uint32_t N = h->cfg.num_procs, P = h->seg;
-    if (num_systems != h->cfg.num_systems) return fail(h, DASH_EINVAL, "num_systems mismatch");
-    for (uint64_t i = 0; i < num_systems * N; i++)
-        if (lens[i] > h->cfg.max_instr || lens[i] > stride)
-            return fail(h, DASH_EINVAL, "trace %llu longer than max_instr", (unsigned long long)i);
-    // the 3-bit node field cannot name a node >= 8, so only N < 8 needs the address scan
-    if (N < 8)
-        for (uint64_t r = 0; r < num_systems * N; r++)
-            for (uint32_t i = 0; i < lens[r]; i++) {
-                const uint16_t w = packed[r * stride + i];
-                if (((w >> 12) & 7u) >= N)
-                    return fail(h, DASH_EADDR, "system %llu node %u: address 0x%02X homed on node >= %u",
-                                (unsigned long long)(r / N), (unsigned)(r % N), (w >> 8) & 0x7F, N);
+    return guarded(h, "dash_load_traces", [&]() -> int {
+        if (!h || (!packed && num_systems) || !lens) return DASH_EINVAL;
+        const uint32_t N = h->cfg.num_procs, P = h->seg;
+        if (num_systems != h->cfg.num_systems) return fail(h, DASH_EINVAL, "num_systems mismatch");
+        for (uint64_t i = 0; i < num_systems * N; i++)
+            if (lens[i] > h->cfg.max_instr || lens[i] > stride)
+                return fail(h, DASH_EINVAL, "trace %llu longer than max_instr", (unsigned long long)i);
+        // the 3-bit node field cannot name a node >= 8, so only N < 8 needs the address scan
+        if (N < 8)
+            for (uint64_t r = 0; r < num_systems * N; r++)
+                for (uint32_t i = 0; i < lens[r]; i++) {
+                    const uint16_t w = packed[r * stride + i];
+                    if (((w >> 12) & 7u) >= N)
+                        return fail(h, DASH_EADDR, "system %llu node %u: address 0x%02X homed on node >= %u",
+                                    (unsigned long long)(r / N), (unsigned)(r % N), (w >> 8) & 0x7F, N);
+                }
+        // lane-contiguous layout: [group][lane][chunk][4 x u16]
+        const uint64_t words = h->groups * (uint64_t)h->nchunks * 64;
+        constexpr uint32_t C = dash::CHUNK_INSTR;
+        const uint64_t pitch = (uint64_t)h->nchunks * 8;  // lane stride in bytes
+        HIPCHK(h, hipSetDevice(h->cfg.device));
+        if (P == N) {
+            // system s node t is lane row s*N + t in both layouts: one strided H2D copy, no
+            // host staging. Words past a node's length are never issued (the kernel's pc < len
+            // guard), so they need no zeroing.
+            if (num_systems)
+                HIPCHK(h, hipMemcpy2DAsync(h->d_trace, pitch, packed, stride * 2, std::min<uint64_t>(stride * 2, pitch),
+                                           num_systems * N, hipMemcpyHostToDevice, h->stream));
+        } else {
+            std::vector<uint16_t> host(words * C, 0);
+            for (uint64_t s = 0; s < num_systems; s++) {
+                const uint64_t g = s / (64 / P);
+                const uint32_t lane0 = (uint32_t)(s % (64 / P)) * P;
+                for (uint32_t t = 0; t < N; t++) {
+                    const uint16_t* src = packed + (s * N + t) * stride;
+                    for (uint32_t i = 0; i < lens[s * N + t]; i++)
+                        host[((g * 64 + lane0 + t) * h->nchunks + i / C) * C + (i % C)] = src[i];
+                }
             }
-    // lane-contiguous layout: [group][lane][chunk][4 x u16]
-    const uint64_t words = h->groups * (uint64_t)h->nchunks * 64;
-    constexpr uint32_t C = dash::CHUNK_INSTR;
-    const uint64_t pitch = (uint64_t)h->nchunks * 8;  // lane stride in bytes
-    HIPCHK(h, hipSetDevice(h->cfg.device));
-    if (P == N) {
-        // system s node t is lane row s*N + t in both layouts: one strided H2D copy, no
-        // host staging. Words past a node's length are never issued (the kernel's pc < len
-        // guard), so they need no zeroing.
-        if (num_systems)
-            HIPCHK(h, hipMemcpy2DAsync(h->d_trace, pitch, packed, stride * 2, std::min<uint64_t>(stride * 2, pitch),
-                                       num_systems * N, hipMemcpyHostToDevice, h->stream));
-    } else {
-        std::vector<uint16_t> host(words * C, 0);
-        for (uint64_t s = 0; s < num_systems; s++) {
-            const uint64_t g = s / (64 / P);
-            const uint32_t lane0 = (uint32_t)(s % (64 / P)) * P;
-            for (uint32_t t = 0; t < N; t++) {
-                const uint16_t* src = packed + (s * N + t) * stride;
-                for (uint32_t i = 0; i < lens[s * N + t]; i++)
-                    host[((g * 64 + lane0 + t) * h->nchunks + i / C) * C + (i % C)] = src[i];
-            }
+            if (words)
+                HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 8, hipMemcpyHostToDevice, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));  // `host` is pageable and local
         }
-        if (words)
-            HIPCHK(h, hipMemcpyAsync(h->d_trace, host.data(), words * 8, hipMemcpyHostToDevice, h->stream));
-        HIPCHK(h, hipStreamSynchronize(h->stream));  // `host` is pageable and local
-    }
-    // RD carries value 0 whatever the caller's bits 7..0 say (ref :839; dash.h)
-    HIPCHK(h, dash::launch_clear_rd(h->d_trace, words, h->stream));
-    if (num_systems)
-        HIPCHK(h, hipMemcpyAsync(h->d_lens, lens, num_systems * N * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, reset_hint(h));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    h->loaded = true;
-    h->ran = false;
-    return DASH_OK;
+        // RD carries value 0 whatever the caller's bits 7..0 say (ref :839; dash.h)
+        HIPCHK(h, dash::launch_clear_rd(h->d_trace, words, h->stream));
+        if (num_systems)
+            HIPCHK(h, hipMemcpyAsync(h->d_lens, lens, num_systems * N * 4, hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, reset_hint(h));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->loaded = true;
+        h->ran = false;
+        return DASH_OK;
+    });
 }
 
 int dash_generate(dash_t* h, const dash_gen* g) {
@@ -319,41 +342,43 @@ int dash_generate(dash_t* h, const dash_gen* g) {
 }
 
 int dash_set_schedule(dash_t* h, const uint8_t* sched, uint32_t rounds) {
-    if (!h || (!sched && rounds)) return DASH_EINVAL;
-    if (!h->d_arb) return fail(h, DASH_ESTATE, "dash_set_schedule: handle created with schedule_seed = 0");
-    const uint32_t N = h->cfg.num_procs, P = h->seg;
-    if (h->arb_len < h->cfg.max_rounds)
-        return fail(h, DASH_EINVAL, "dash_set_schedule: the round table holds %u of max_rounds %llu rounds",
-                    h->arb_len, (unsigned long long)h->cfg.max_rounds);
-    if (rounds > h->arb_len) return fail(h, DASH_EINVAL, "dash_set_schedule: %u rounds > max_rounds", rounds);
-    for (uint32_t r = 0; r < rounds; r++) {
-        uint32_t used = 0;
-        for (uint32_t t = 0; t < N; t++) {
-            const uint8_t v = sched[(uint64_t)r * N + t];
-            if (v == DASH_SIT_OUT) continue;
-            if (v >= P || (used >> v) & 1u)
-                return fail(h, DASH_EINVAL, "dash_set_schedule: round %u node %u: position %u invalid or repeated",
-                            r, t, (unsigned)v);
-            used |= 1u << v;
-        }
-    }
-    // the kernel's table layout (dash_kernels.hip arb_table_kernel): [round / 4][lane][round % 4],
-    // each word 0 for a node sitting out, else its primary arrival bit 2 << 4 * position
-    std::vector<uint32_t> tab(((uint64_t)h->arb_len + 4) * P, 0);
-    for (uint64_t r = 0; r < (uint64_t)h->arb_len + 4; r++)
-        for (uint32_t t = 0; t < P; t++) {
-            uint32_t w = 0;
-            if (t < N) {
-                const uint32_t v = r < rounds ? sched[r * N + t] : t;  // later rounds: lockstep
-                w = v == DASH_SIT_OUT ? 0u : 2u << (4u * v);
+    return guarded(h, "dash_set_schedule", [&]() -> int {
+        if (!h || (!sched && rounds)) return DASH_EINVAL;
+        if (!h->d_arb) return fail(h, DASH_ESTATE, "dash_set_schedule: handle created with schedule_seed = 0");
+        const uint32_t N = h->cfg.num_procs, P = h->seg;
+        if (h->arb_len < h->cfg.max_rounds)
+            return fail(h, DASH_EINVAL, "dash_set_schedule: the round table holds %u of max_rounds %llu rounds",
+                        h->arb_len, (unsigned long long)h->cfg.max_rounds);
+        if (rounds > h->arb_len) return fail(h, DASH_EINVAL, "dash_set_schedule: %u rounds > max_rounds", rounds);
+        for (uint32_t r = 0; r < rounds; r++) {
+            uint32_t used = 0;
+            for (uint32_t t = 0; t < N; t++) {
+                const uint8_t v = sched[(uint64_t)r * N + t];
+                if (v == DASH_SIT_OUT) continue;
+                if (v >= P || (used >> v) & 1u)
+                    return fail(h, DASH_EINVAL, "dash_set_schedule: round %u node %u: position %u invalid or repeated",
+                                r, t, (unsigned)v);
+                used |= 1u << v;
             }
-            tab[((r >> 2) * P + t) * 4 + (r & 3)] = w;
         }
-    HIPCHK(h, hipSetDevice(h->cfg.device));
-    HIPCHK(h, hipMemcpyAsync(h->d_arb, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    h->ran = false;
-    return DASH_OK;
+        // the kernel's table layout (dash_kernels.hip arb_table_kernel): [round / 4][lane][round % 4],
+        // each word 0 for a node sitting out, else its primary arrival bit 2 << 4 * position
+        std::vector<uint32_t> tab(((uint64_t)h->arb_len + 4) * P, 0);
+        for (uint64_t r = 0; r < (uint64_t)h->arb_len + 4; r++)
+            for (uint32_t t = 0; t < P; t++) {
+                uint32_t w = 0;
+                if (t < N) {
+                    const uint32_t v = r < rounds ? sched[r * N + t] : t;  // later rounds: lockstep
+                    w = v == DASH_SIT_OUT ? 0u : 2u << (4u * v);
+                }
+                tab[((r >> 2) * P + t) * 4 + (r & 3)] = w;
+            }
+        HIPCHK(h, hipSetDevice(h->cfg.device));
+        HIPCHK(h, hipMemcpyAsync(h->d_arb, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->ran = false;
+        return DASH_OK;
+    });
 }
 
 int dash_run(dash_t* h, dash_stats* stats) {
@@ -499,33 +524,35 @@ int dash_read_results(dash_t* h, uint64_t first, uint64_t count, uint64_t* diges
 }
 
 int dash_read_state(dash_t* h, uint64_t sys, dash_node_state* out) {
-    if (!h || !out) return DASH_EINVAL;
-    if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
-    if (!h->d_state) return fail(h, DASH_ESTATE, "created without DASH_KEEP_STATE");
-    if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
-    const uint32_t N = h->cfg.num_procs, CS = h->cfg.cache_size, W = 16 + CS;
-    std::vector<uint32_t> w((size_t)N * W);
-    HIPCHK(h, hipSetDevice(h->cfg.device));
-    HIPCHK(h, hipMemcpyAsync(w.data(), h->d_state + sys * N * W, w.size() * 4, hipMemcpyDeviceToHost,
-                             h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    for (uint32_t t = 0; t < N; t++) {
-        dash_node_state* s = &out[t];
-        memset(s, 0, sizeof *s);
-        for (uint32_t b = 0; b < 16; b++) {
-            const uint32_t e = w[t * W + b];
-            s->memory[b] = (uint8_t)(e & 0xFF);
-            s->dir_bitvector[b] = (uint8_t)((e >> 8) & 0xFF);
-            s->dir_state[b] = (uint8_t)((e >> 16) & 3);
+    return guarded(h, "dash_read_state", [&]() -> int {
+        if (!h || !out) return DASH_EINVAL;
+        if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
+        if (!h->d_state) return fail(h, DASH_ESTATE, "created without DASH_KEEP_STATE");
+        if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
+        const uint32_t N = h->cfg.num_procs, CS = h->cfg.cache_size, W = 16 + CS;
+        std::vector<uint32_t> w((size_t)N * W);
+        HIPCHK(h, hipSetDevice(h->cfg.device));
+        HIPCHK(h, hipMemcpyAsync(w.data(), h->d_state + sys * N * W, w.size() * 4, hipMemcpyDeviceToHost,
+                                 h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        for (uint32_t t = 0; t < N; t++) {
+            dash_node_state* s = &out[t];
+            memset(s, 0, sizeof *s);
+            for (uint32_t b = 0; b < 16; b++) {
+                const uint32_t e = w[t * W + b];
+                s->memory[b] = (uint8_t)(e & 0xFF);
+                s->dir_bitvector[b] = (uint8_t)((e >> 8) & 0xFF);
+                s->dir_state[b] = (uint8_t)((e >> 16) & 3);
+            }
+            for (uint32_t i = 0; i < CS; i++) {
+                const uint32_t l = w[t * W + 16 + i];
+                s->cache_addr[i] = (uint8_t)(l & 0xFF);
+                s->cache_value[i] = (uint8_t)((l >> 8) & 0xFF);
+                s->cache_state[i] = (uint8_t)((l >> 16) & 3);
+            }
         }
-        for (uint32_t i = 0; i < CS; i++) {
-            const uint32_t l = w[t * W + 16 + i];
-            s->cache_addr[i] = (uint8_t)(l & 0xFF);
-            s->cache_value[i] = (uint8_t)((l >> 8) & 0xFF);
-            s->cache_state[i] = (uint8_t)((l >> 16) & 3);
-        }
-    }
-    return DASH_OK;
+        return DASH_OK;
+    });
 }
 
 int dash_read_hist(dash_t* h, uint64_t sys, uint32_t* hist) {
@@ -541,208 +568,319 @@ int dash_read_hist(dash_t* h, uint64_t sys, uint32_t* hist) {
 }
 
 int dash_read_events(dash_t* h, uint64_t sys, dash_event* out, uint32_t cap, uint32_t* n) {
-    if (!h || (!out && cap) || !n) return DASH_EINVAL;
-    if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
-    if (!h->d_events) return fail(h, DASH_ESTATE, "created with trace_events = 0");
-    if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
-    const uint32_t N = h->cfg.num_procs, E = h->cfg.trace_events;
-    std::vector<uint32_t> cnt(N), ev((size_t)N * E * 2);
-    HIPCHK(h, hipSetDevice(h->cfg.device));
-    HIPCHK(h, hipMemcpyAsync(cnt.data(), h->d_event_count + sys * N, N * 4, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(h, hipMemcpyAsync(ev.data(), h->d_events + sys * N * E * 2, ev.size() * 4, hipMemcpyDeviceToHost,
-                             h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    // merge the per-node logs (each in round order) by (round, node): a node logs at
-    // most one event per round, so this is the lockstep order
-    std::vector<uint32_t> pos(N, 0);
-    bool trunc = false;
-    uint64_t total = 0;
-    for (uint32_t t = 0; t < N; t++) {
-        total += cnt[t];
-        if (cnt[t] > E) trunc = true;
-    }
-    uint32_t k = 0;
-    for (;;) {
-        int best = -1;
+    return guarded(h, "dash_read_events", [&]() -> int {
+        if (!h || (!out && cap) || !n) return DASH_EINVAL;
+        if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
+        if (!h->d_events) return fail(h, DASH_ESTATE, "created with trace_events = 0");
+        if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
+        const uint32_t N = h->cfg.num_procs, E = h->cfg.trace_events;
+        std::vector<uint32_t> cnt(N), ev((size_t)N * E * 2);
+        HIPCHK(h, hipSetDevice(h->cfg.device));
+        HIPCHK(h, hipMemcpyAsync(cnt.data(), h->d_event_count + sys * N, N * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(ev.data(), h->d_events + sys * N * E * 2, ev.size() * 4, hipMemcpyDeviceToHost,
+                                 h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        // merge the per-node logs (each in round order) by (round, node): a node logs at
+        // most one event per round, so this is the lockstep order
+        std::vector<uint32_t> pos(N, 0);
+        bool trunc = false;
+        uint64_t total = 0;
         for (uint32_t t = 0; t < N; t++) {
-            if (pos[t] >= std::min(cnt[t], E)) continue;
-            if (best < 0 || (ev[((size_t)t * E + pos[t]) * 2] & 0x7FFFFFFFu) <
-                                (ev[((size_t)best * E + pos[best]) * 2] & 0x7FFFFFFFu))
-                best = (int)t;
+            total += cnt[t];
+            if (cnt[t] > E) trunc = true;
         }
-        if (best < 0) break;
-        const uint32_t* e = &ev[((size_t)best * E + pos[best]) * 2];
-        if (k < cap) {
-            out[k].round = e[0] & 0x7FFFFFFFu;  // bit 31: an issued instruction
-            out[k].node = (uint32_t)best;
-            out[k].kind = (e[0] & 0x80000000u) ? DASH_EV_INSTR : DASH_EV_MSG;
-            // a message word without the kernel's internal bits (7: REPLY_RD's dirState,
-            // 15: the reply-table flag, 27..24) and with secondReceiver moved from bits 30..28
-            // to 26..24, as include/dash.h documents it
-            out[k].word = (e[0] & 0x80000000u) ? e[1] : (e[1] & 0x00FF7F7Fu) | (((e[1] >> 28) & 7u) << 24);
+        uint32_t k = 0;
+        for (;;) {
+            int best = -1;
+            for (uint32_t t = 0; t < N; t++) {
+                if (pos[t] >= std::min(cnt[t], E)) continue;
+                if (best < 0 || (ev[((size_t)t * E + pos[t]) * 2] & 0x7FFFFFFFu) <
+                                    (ev[((size_t)best * E + pos[best]) * 2] & 0x7FFFFFFFu))
+                    best = (int)t;
+            }
+            if (best < 0) break;
+            const uint32_t* e = &ev[((size_t)best * E + pos[best]) * 2];
+            if (k < cap) {
+                out[k].round = e[0] & 0x7FFFFFFFu;  // bit 31: an issued instruction
+                out[k].node = (uint32_t)best;
+                out[k].kind = (e[0] & 0x80000000u) ? DASH_EV_INSTR : DASH_EV_MSG;
+                // a message word without the kernel's internal bits (7: REPLY_RD's dirState,
+                // 15: the reply-table flag, 27..24) and with secondReceiver moved from bits 30..28
+                // to 26..24, as include/dash.h documents it
+                out[k].word = (e[0] & 0x80000000u) ? e[1] : (e[1] & 0x00FF7F7Fu) | (((e[1] >> 28) & 7u) << 24);
+            }
+            ++k;
+            ++pos[best];
         }
-        ++k;
-        ++pos[best];
-    }
-    *n = (uint32_t)std::min<uint64_t>(total, 0xFFFFFFFFull);
-    return trunc ? fail(h, DASH_ETRUNC, "event log truncated at %u events per node", E) : DASH_OK;
+        *n = (uint32_t)std::min<uint64_t>(total, 0xFFFFFFFFull);
+        return trunc ? fail(h, DASH_ETRUNC, "event log truncated at %u events per node", E) : DASH_OK;
+    });
 }
 
 int dash_load_dir(dash_t* h, const char* dir, uint64_t sys) {
-    if (!h || !dir) return DASH_EINVAL;
-    if (h->cfg.num_systems != 1 || sys != 0)
-        return fail(h, DASH_EINVAL, "dash_load_dir loads a batch of one system");
-    char base[4096], path[4200];
-    int rc = dash_resolve_dir(dir, base, sizeof base);
-    const uint32_t N = h->cfg.num_procs, M = h->cfg.max_instr;
-    std::vector<uint16_t> tr((size_t)N * std::max<uint32_t>(M, 1), 0);
-    std::vector<uint32_t> lens(N, 0);
-    for (uint32_t t = 0; t < N; t++) {
-        snprintf(path, sizeof path, "%s/core_%u.txt", base, t);
-        rc = dash_parse_core_file(path, N, M, tr.data() + (size_t)t * std::max<uint32_t>(M, 1), &lens[t]);
-        if (rc != DASH_OK) return fail(h, rc, "%s: parse failed (%d)", path, rc);
-        printf("Processor %u initialized\n", t); /* ref :850 */
-    }
-    return dash_load_traces(h, tr.data(), std::max<uint32_t>(M, 1), lens.data(), 1);
+    return guarded(h, "dash_load_dir", [&]() -> int {
+        if (!h || !dir) return DASH_EINVAL;
+        if (h->cfg.num_systems != 1 || sys != 0)
+            return fail(h, DASH_EINVAL, "dash_load_dir loads a batch of one system");
+        char base[4096], path[4200];
+        int rc = dash_resolve_dir(dir, base, sizeof base);
+        const uint32_t N = h->cfg.num_procs, M = h->cfg.max_instr;
+        std::vector<uint16_t> tr((size_t)N * std::max<uint32_t>(M, 1), 0);
+        std::vector<uint32_t> lens(N, 0);
+        for (uint32_t t = 0; t < N; t++) {
+            snprintf(path, sizeof path, "%s/core_%u.txt", base, t);
+            rc = dash_parse_core_file(path, N, M, tr.data() + (size_t)t * std::max<uint32_t>(M, 1), &lens[t]);
+            if (rc != DASH_OK) return fail(h, rc, "%s: parse failed (%d)", path, rc);
+            printf("Processor %u initialized\n", t); /* ref :850 */
+        }
+        return dash_load_traces(h, tr.data(), std::max<uint32_t>(M, 1), lens.data(), 1);
+    });
 }
 
 int dash_load_dirs(dash_t* h, const char* const* dirs, uint64_t n) {
-    if (!h || (!dirs && n)) return DASH_EINVAL;
-    if (n != h->cfg.num_systems) return fail(h, DASH_EINVAL, "%llu directories for %llu systems",
-                                             (unsigned long long)n, (unsigned long long)h->cfg.num_systems);
-    const uint32_t N = h->cfg.num_procs, M = h->cfg.max_instr, stride = std::max<uint32_t>(M, 1);
-    std::vector<uint16_t> tr((size_t)n * N * stride, 0);
-    std::vector<uint32_t> lens((size_t)n * N, 0);
-    std::atomic<uint64_t> next{0}, bad{~0ull};
-    std::atomic<int> bad_rc{DASH_OK};
-    auto worker = [&]() {
-        char base[4096], path[4200];
-        for (uint64_t k; (k = next.fetch_add(1)) < n;) {
-            int rc = dash_resolve_dir(dirs[k], base, sizeof base);
-            for (uint32_t t = 0; rc == DASH_OK && t < N; t++) {
-                snprintf(path, sizeof path, "%s/core_%u.txt", base, t);
-                rc = dash_parse_core_file(path, N, M, tr.data() + (k * N + t) * stride, &lens[k * N + t]);
-            }
-            if (rc != DASH_OK) {
-                uint64_t prev = bad.load();
-                while (k < prev && !bad.compare_exchange_weak(prev, k)) {
+    return guarded(h, "dash_load_dirs", [&]() -> int {
+        if (!h || (!dirs && n)) return DASH_EINVAL;
+        if (n != h->cfg.num_systems) return fail(h, DASH_EINVAL, "%llu directories for %llu systems",
+                                                 (unsigned long long)n, (unsigned long long)h->cfg.num_systems);
+        const uint32_t N = h->cfg.num_procs, M = h->cfg.max_instr, stride = std::max<uint32_t>(M, 1);
+        std::vector<uint16_t> tr((size_t)n * N * stride, 0);
+        std::vector<uint32_t> lens((size_t)n * N, 0);
+        std::atomic<uint64_t> next{0}, bad{~0ull};
+        std::atomic<int> bad_rc{DASH_OK};
+        auto worker = [&]() {
+            char base[4096], path[4200];
+            for (uint64_t k; (k = next.fetch_add(1)) < n;) {
+                int rc = dash_resolve_dir(dirs[k], base, sizeof base);
+                for (uint32_t t = 0; rc == DASH_OK && t < N; t++) {
+                    snprintf(path, sizeof path, "%s/core_%u.txt", base, t);
+                    rc = dash_parse_core_file(path, N, M, tr.data() + (k * N + t) * stride, &lens[k * N + t]);
                 }
-                bad_rc = rc;
+                if (rc != DASH_OK) {
+                    uint64_t prev = bad.load();
+                    while (k < prev && !bad.compare_exchange_weak(prev, k)) {
+                    }
+                    bad_rc = rc;
+                }
             }
+        };
+        const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({n, 16, std::max(1u, std::thread::hardware_concurrency())}));
+        std::vector<std::thread> pool;
+        try {
+            for (unsigned i = 1; i < nt; i++) pool.emplace_back(worker);
+        } catch (...) {  // no thread: the calling thread takes the remaining directories
         }
-    };
-    const unsigned nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>({n, 16, std::max(1u, std::thread::hardware_concurrency())}));
-    std::vector<std::thread> pool;
-    try {
-        for (unsigned i = 1; i < nt; i++) pool.emplace_back(worker);
-    } catch (...) {  // no thread: the calling thread takes the remaining directories
-    }
-    worker();
-    for (auto& th : pool) th.join();
-    if (bad.load() != ~0ull)
-        return fail(h, bad_rc.load(), "%s: trace directory rejected (%d)", dirs[bad.load()], bad_rc.load());
-    return dash_load_traces(h, tr.data(), stride, lens.data(), n);
+        worker();
+        for (auto& th : pool) th.join();
+        if (bad.load() != ~0ull)
+            return fail(h, bad_rc.load(), "%s: trace directory rejected (%d)", dirs[bad.load()], bad_rc.load());
+        return dash_load_traces(h, tr.data(), stride, lens.data(), n);
+    });
 }
 
 int dash_dump_system(dash_t* h, uint64_t sys, const char* out_dir) {
-    if (!h || !out_dir) return DASH_EINVAL;
-    std::vector<dash_node_state> st(h->cfg.num_procs);
-    int rc = dash_read_state(h, sys, st.data());
-    if (rc != DASH_OK) return rc;
-    if (mkdir(out_dir, 0755) != 0 && errno != EEXIST) return fail(h, DASH_EIO, "mkdir %s", out_dir);
-    for (uint32_t t = 0; t < h->cfg.num_procs; t++) {
-        char path[4200];
-        snprintf(path, sizeof path, "%s/core_%u_output.txt", out_dir, t);
-        rc = dash_dump_file(&st[t], t, h->cfg.cache_size, path);
-        if (rc != DASH_OK) return fail(h, rc, "write %s", path);
+    return guarded(h, "dash_dump_system", [&]() -> int {
+        if (!h || !out_dir) return DASH_EINVAL;
+        std::vector<dash_node_state> st(h->cfg.num_procs);
+        int rc = dash_read_state(h, sys, st.data());
+        if (rc != DASH_OK) return rc;
+        if (mkdir(out_dir, 0755) != 0 && errno != EEXIST) return fail(h, DASH_EIO, "mkdir %s", out_dir);
+        for (uint32_t t = 0; t < h->cfg.num_procs; t++) {
+            char path[4200];
+            snprintf(path, sizeof path, "%s/core_%u_output.txt", out_dir, t);
+            rc = dash_dump_file(&st[t], t, h->cfg.cache_size, path);
+            if (rc != DASH_OK) return fail(h, rc, "write %s", path);
+        }
+        return DASH_OK;
+    });
+}
+
+// dash_write_digests: the lines of fprintf("%llu %016llx %u %x\n") for every system, formatted by
+// hand in parallel chunks (one fprintf per line ran at ~4e6 lines/s) and written in order. The
+// results are read and formatted one window of chunks (2 per thread) at a time, into buffers
+// reused from window to window, so host memory stays bounded (~8 MiB of text per thread) at
+// any num_systems.
+static int write_digests_impl(dash_t* h, const char* path) {
+    const uint64_t n = h->cfg.num_systems;
+    constexpr uint64_t CHUNK = 1u << 16;  // lines per chunk: <= 64 B each
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint64_t window = std::max<uint64_t>(1, std::min<uint64_t>(n, 2ull * nt * CHUNK));
+    std::vector<uint64_t> d(window);
+    std::vector<uint32_t> r(window), e(window);
+    const uint64_t wch = (window + CHUNK - 1) / CHUNK;
+    std::vector<std::vector<char>> buf(wch);
+    for (auto& b : buf) b.resize(CHUNK * 64);
+    std::vector<size_t> used(wch);
+    FILE* f = fopen(path, "w");
+    if (!f) return fail(h, DASH_EIO, "open %s", path);
+    bool ok = true;
+    for (uint64_t w0 = 0; ok && w0 < n; w0 += window) {
+        const uint64_t wn = std::min(window, n - w0);
+        int rc = dash_read_results(h, w0, wn, d.data(), r.data(), e.data());
+        if (rc != DASH_OK) {
+            fclose(f);
+            return rc;
+        }
+        const uint64_t nch = (wn + CHUNK - 1) / CHUNK;
+        std::atomic<uint64_t> next{0};
+        auto work = [&] {  // touches only its chunks' preallocated buffers: nothing here allocates
+            static const char HEX[] = "0123456789abcdef";
+            for (uint64_t c; (c = next.fetch_add(1)) < nch;) {
+                char* o = buf[c].data();
+                auto dec = [&o](uint64_t v) {
+                    char t[20];
+                    int m = 0;
+                    do t[m++] = (char)('0' + v % 10); while ((v /= 10) != 0);
+                    while (m) *o++ = t[--m];
+                };
+                for (uint64_t k = c * CHUNK; k < std::min<uint64_t>(wn, (c + 1) * CHUNK); k++) {
+                    dec(w0 + k);
+                    *o++ = ' ';
+                    for (int sh = 60; sh >= 0; sh -= 4) *o++ = HEX[(d[k] >> sh) & 15];
+                    *o++ = ' ';
+                    dec(r[k]);
+                    *o++ = ' ';
+                    int sh = 28;
+                    while (sh > 0 && ((e[k] >> sh) & 15) == 0) sh -= 4;
+                    for (; sh >= 0; sh -= 4) *o++ = HEX[(e[k] >> sh) & 15];
+                    *o++ = '\n';
+                }
+                used[c] = (size_t)(o - buf[c].data());
+            }
+        };
+        std::vector<std::thread> pool;
+        try {
+            for (uint64_t i = 1; i < std::min<uint64_t>(nch, nt); i++) pool.emplace_back(work);
+        } catch (...) {  // no thread: the calling thread formats the remaining chunks
+        }
+        work();
+        for (auto& th : pool) th.join();
+        for (uint64_t c = 0; ok && c < nch; c++) ok = fwrite(buf[c].data(), 1, used[c], f) == used[c];
     }
-    return DASH_OK;
+    return (fclose(f) == 0 && ok) ? DASH_OK : fail(h, DASH_EIO, "write %s", path);
 }
 
 int dash_write_digests(dash_t* h, const char* path) {
     if (!h || !path) return DASH_EINVAL;
-    const uint64_t n = h->cfg.num_systems;
-    std::vector<uint64_t> d(n);
-    std::vector<uint32_t> r(n), e(n);
-    int rc = dash_read_results(h, 0, n, d.data(), r.data(), e.data());
-    if (rc != DASH_OK) return rc;
-    FILE* f = fopen(path, "w");
-    if (!f) return fail(h, DASH_EIO, "open %s", path);
-    // the lines of fprintf("%llu %016llx %u %x\n"), formatted by hand in parallel chunks (one
-    // fprintf per line ran at ~4e6 lines/s) and written in order
-    constexpr uint64_t CHUNK = 1u << 16;  // lines per chunk: <= 64 B each
-    const uint64_t nch = (n + CHUNK - 1) / CHUNK;
-    std::vector<std::vector<char>> buf(nch);
-    std::atomic<uint64_t> next{0};
-    auto work = [&] {
-        static const char HEX[] = "0123456789abcdef";
-        for (uint64_t c; (c = next.fetch_add(1)) < nch;) {
-            std::vector<char>& b = buf[c];
-            b.resize(std::min<uint64_t>(CHUNK, n - c * CHUNK) * 64);
-            char* o = b.data();
-            auto dec = [&o](uint64_t v) {
-                char t[20];
-                int m = 0;
-                do t[m++] = (char)('0' + v % 10); while ((v /= 10) != 0);
-                while (m) *o++ = t[--m];
-            };
-            for (uint64_t k = c * CHUNK; k < std::min<uint64_t>(n, (c + 1) * CHUNK); k++) {
-                dec(k);
-                *o++ = ' ';
-                for (int sh = 60; sh >= 0; sh -= 4) *o++ = HEX[(d[k] >> sh) & 15];
-                *o++ = ' ';
-                dec(r[k]);
-                *o++ = ' ';
-                int sh = 28;
-                while (sh > 0 && ((e[k] >> sh) & 15) == 0) sh -= 4;
-                for (; sh >= 0; sh -= 4) *o++ = HEX[(e[k] >> sh) & 15];
-                *o++ = '\n';
-            }
-            b.resize((size_t)(o - b.data()));
-        }
-    };
-    const uint64_t nt = std::min<uint64_t>(nch, std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
-    std::vector<std::thread> pool;
-    try {
-        for (uint64_t i = 1; i < nt; i++) pool.emplace_back(work);
-    } catch (...) {  // no thread: the calling thread formats the remaining chunks
+    try {  // no C++ exception crosses the C-ABI
+        return write_digests_impl(h, path);
+    } catch (const std::bad_alloc&) {
+        return fail(h, DASH_ENOMEM, "dash_write_digests: out of host memory");
+    } catch (...) {
+        return fail(h, DASH_EIO, "dash_write_digests: unexpected failure");
     }
-    work();
-    for (auto& th : pool) th.join();
-    bool ok = true;
-    for (auto& b : buf) ok = ok && fwrite(b.data(), 1, b.size(), f) == b.size();
-    return (fclose(f) == 0 && ok) ? DASH_OK : fail(h, DASH_EIO, "write %s", path);
+}
+
+int dash_probe_box(int device, dash_box_probe* out) {
+    return guarded(nullptr, "dash_probe_box", [&]() -> int {
+        set_global_msg("");
+        if (!out) return DASH_EINVAL;
+        memset(out, 0, sizeof *out);
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+            set_global_msg("dash_probe_box: no such HIP device");
+            return DASH_EDEVICE;
+        }
+        hipDeviceProp_t p;
+        if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&p, device) != hipSuccess) {
+            set_global_msg("dash_probe_box: hipGetDeviceProperties failed");
+            return DASH_EDEVICE;
+        }
+        snprintf(out->name, sizeof out->name, "%s", p.name);
+        if (!out->name[0] && hipDeviceGetName(out->name, (int)sizeof out->name, device) != hipSuccess) out->name[0] = 0;
+        snprintf(out->arch, sizeof out->arch, "%s", p.gcnArchName);
+        out->compute_units = p.multiProcessorCount;
+        out->clock_khz = p.clockRate;
+        out->mem_clock_khz = p.memoryClockRate;
+        out->pci_domain = p.pciDomainID;
+        out->pci_bus = p.pciBusID;
+        out->pci_device = p.pciDeviceID;
+        out->total_mem = p.totalGlobalMem;
+        const uint32_t blocks = (uint32_t)std::max(1, p.multiProcessorCount) * 8u;
+        const uint32_t iters = 1u << 18;  // ~100 ms at 2.4 GHz
+        uint32_t* sink = nullptr;
+        unsigned long long* clk = nullptr;
+        hipStream_t st = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        int rc = DASH_OK;
+        auto chk = [&](hipError_t e, const char* what) {
+            if (e != hipSuccess && rc == DASH_OK) {
+                rc = DASH_EDEVICE;
+                char m[256];
+                snprintf(m, sizeof m, "dash_probe_box: %s: %s", what, hipGetErrorString(e));
+                set_global_msg(m);
+            }
+        };
+        chk(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "stream");
+        chk(hipEventCreate(&e0), "event");
+        chk(hipEventCreate(&e1), "event");
+        chk(hipMalloc(&sink, 4), "hipMalloc");
+        chk(hipMalloc(&clk, (size_t)blocks * 2 * sizeof(unsigned long long)), "hipMalloc");
+        if (rc == DASH_OK) chk(dash::launch_probe(blocks, 1024, sink, clk, st), "warm-up launch");
+        if (rc == DASH_OK) chk(hipEventRecord(e0, st), "event");
+        if (rc == DASH_OK) chk(dash::launch_probe(blocks, iters, sink, clk, st), "launch");
+        if (rc == DASH_OK) chk(hipEventRecord(e1, st), "event");
+        std::vector<unsigned long long> c((size_t)blocks * 2);
+        if (rc == DASH_OK) chk(hipMemcpyAsync(c.data(), clk, c.size() * sizeof(c[0]), hipMemcpyDeviceToHost, st), "copy");
+        if (rc == DASH_OK) chk(hipStreamSynchronize(st), "sync");
+        float ms = 0.f;
+        if (rc == DASH_OK) chk(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+        if (rc == DASH_OK) {
+            double cyc = 0, ref = 0, lo = 1e30, hi = 0;
+            for (uint32_t b = 0; b < blocks; b++) {
+                cyc += (double)c[2 * b];
+                ref += (double)c[2 * b + 1];
+                if (c[2 * b + 1]) {
+                    const double f = (double)c[2 * b] / (double)c[2 * b + 1] * 100.0;  // MHz
+                    lo = std::min(lo, f);
+                    hi = std::max(hi, f);
+                }
+            }
+            out->probe_ms = ms;
+            out->probe_valu_per_s = (double)blocks * 4.0 * iters * dash::PROBE_VALU_PER_TRIP / (ms / 1e3);
+            out->probe_sclk_mhz = ref > 0 ? cyc / ref * 100.0 : 0.0;
+            out->probe_sclk_min_mhz = hi > 0 ? lo : 0.0;
+            out->probe_sclk_max_mhz = hi;
+        }
+        (void)hipFree(sink);
+        (void)hipFree(clk);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (st) (void)hipStreamDestroy(st);
+        return rc;
+    });
 }
 
 int dash_simulate_dir(const char* dir, uint32_t num_procs, uint32_t cache_size, uint32_t max_instr,
                       const char* out_dir, int device, dash_stats* stats) {
-    dash_cfg cfg{};
-    cfg.num_procs = num_procs;
-    cfg.cache_size = cache_size;
-    cfg.max_instr = max_instr;
-    cfg.flags = DASH_KEEP_STATE;
-    cfg.num_systems = 1;
-    cfg.device = device;
-    dash_t* h = nullptr;
-    int rc = dash_create(&cfg, &h);
-    if (rc != DASH_OK) return rc;
-    rc = dash_load_dir(h, dir, 0);
-    if (rc != DASH_OK) {
-        set_global_msg(h->msg);
+    return guarded(nullptr, "dash_simulate_dir", [&]() -> int {
+        dash_cfg cfg{};
+        cfg.num_procs = num_procs;
+        cfg.cache_size = cache_size;
+        cfg.max_instr = max_instr;
+        cfg.flags = DASH_KEEP_STATE;
+        cfg.num_systems = 1;
+        cfg.device = device;
+        dash_t* h = nullptr;
+        int rc = dash_create(&cfg, &h);
+        if (rc != DASH_OK) return rc;
+        rc = dash_load_dir(h, dir, 0);
+        if (rc != DASH_OK) {
+            set_global_msg(h->msg);
+            dash_destroy(h);
+            return rc;
+        }
+        rc = dash_run(h, stats);
+        std::vector<dash_node_state> st(num_procs);
+        if (rc == DASH_OK) rc = dash_read_state(h, 0, st.data());
+        for (uint32_t t = 0; rc == DASH_OK && t < num_procs; t++) {
+            char path[4200];
+            snprintf(path, sizeof path, "%s/core_%u_output.txt", out_dir ? out_dir : ".", t);
+            rc = dash_dump_file(&st[t], t, cache_size, path);
+        }
+        if (rc != DASH_OK) set_global_msg(h->msg);
         dash_destroy(h);
         return rc;
-    }
-    rc = dash_run(h, stats);
-    std::vector<dash_node_state> st(num_procs);
-    if (rc == DASH_OK) rc = dash_read_state(h, 0, st.data());
-    for (uint32_t t = 0; rc == DASH_OK && t < num_procs; t++) {
-        char path[4200];
-        snprintf(path, sizeof path, "%s/core_%u_output.txt", out_dir ? out_dir : ".", t);
-        rc = dash_dump_file(&st[t], t, cache_size, path);
-    }
-    if (rc != DASH_OK) set_global_msg(h->msg);
-    dash_destroy(h);
-    return rc;
+    });
 }
 
 }  // extern "C"
@@ -752,84 +890,86 @@ extern "C" int dash_run_host_batched(const dash_cfg* cfg, const uint16_t* packed
                                      const uint32_t* lens, uint64_t num_systems, uint32_t batches,
                                      dash_stats* stats, uint64_t* digests, uint32_t* rounds,
                                      uint32_t* errors) {
-    if (!cfg || !packed || !lens || !stats || batches == 0 || num_systems == 0 || num_systems % batches)
-        return DASH_EINVAL;
-    const uint64_t nb = num_systems / batches, N = cfg->num_procs;
-    dash_cfg c = *cfg;
-    c.num_systems = nb;
-    // throughput path: per-system state snapshots and event logs are not returned here,
-    // so the handles do not allocate them
-    c.flags &= ~(uint32_t)DASH_KEEP_STATE;
-    c.trace_events = 0;
-    const unsigned nh = batches < 2 ? 1u : 2u;
-    dash_t* h[2] = {nullptr, nullptr};
-    set_global_msg("");
-    int rc = DASH_OK;
-    for (unsigned i = 0; i < nh && rc == DASH_OK; i++) rc = dash_create(&c, &h[i]);
-    dash_stats part[2];
-    memset(part, 0, sizeof part);
-    int trc[2] = {DASH_OK, DASH_OK};
-    std::atomic<bool> stop{false};  // the first failing lane stops the other one too
-    // handle i (its own HIP stream) takes batches i, i+2, ...: while one copies, the other runs
-    auto lane = [&](unsigned i) {
-        for (uint64_t b = i; b < batches && !stop.load(); b += nh) {
-            int r = dash_load_traces(h[i], packed + b * nb * N * stride, stride, lens + b * nb * N, nb);
-            dash_stats st;
-            if (r == DASH_OK) r = dash_run(h[i], &st);
-            if (r == DASH_OK && (digests || rounds || errors))
-                r = dash_read_results(h[i], 0, nb, digests ? digests + b * nb : nullptr,
-                                      rounds ? rounds + b * nb : nullptr, errors ? errors + b * nb : nullptr);
-            if (r != DASH_OK) {
-                trc[i] = r;
-                stop.store(true);
-                break;
+    return guarded(nullptr, "dash_run_host_batched", [&]() -> int {
+        if (!cfg || !packed || !lens || !stats || batches == 0 || num_systems == 0 || num_systems % batches)
+            return DASH_EINVAL;
+        const uint64_t nb = num_systems / batches, N = cfg->num_procs;
+        dash_cfg c = *cfg;
+        c.num_systems = nb;
+        // throughput path: per-system state snapshots and event logs are not returned here,
+        // so the handles do not allocate them
+        c.flags &= ~(uint32_t)DASH_KEEP_STATE;
+        c.trace_events = 0;
+        const unsigned nh = batches < 2 ? 1u : 2u;
+        dash_t* h[2] = {nullptr, nullptr};
+        set_global_msg("");
+        int rc = DASH_OK;
+        for (unsigned i = 0; i < nh && rc == DASH_OK; i++) rc = dash_create(&c, &h[i]);
+        dash_stats part[2];
+        memset(part, 0, sizeof part);
+        int trc[2] = {DASH_OK, DASH_OK};
+        std::atomic<bool> stop{false};  // the first failing lane stops the other one too
+        // handle i (its own HIP stream) takes batches i, i+2, ...: while one copies, the other runs
+        auto lane = [&](unsigned i) {
+            for (uint64_t b = i; b < batches && !stop.load(); b += nh) {
+                int r = dash_load_traces(h[i], packed + b * nb * N * stride, stride, lens + b * nb * N, nb);
+                dash_stats st;
+                if (r == DASH_OK) r = dash_run(h[i], &st);
+                if (r == DASH_OK && (digests || rounds || errors))
+                    r = dash_read_results(h[i], 0, nb, digests ? digests + b * nb : nullptr,
+                                          rounds ? rounds + b * nb : nullptr, errors ? errors + b * nb : nullptr);
+                if (r != DASH_OK) {
+                    trc[i] = r;
+                    stop.store(true);
+                    break;
+                }
+                dash_stats& p = part[i];
+                for (int k = 0; k < DASH_NUM_TXN; k++) p.hist[k] += st.hist[k];
+                p.instructions += st.instructions;
+                p.rounds_total += st.rounds_total;
+                p.rounds_max = std::max(p.rounds_max, st.rounds_max);
+                p.systems += st.systems;
+                p.err_systems += st.err_systems;
+                p.err_bits |= st.err_bits;
+                p.dropped += st.dropped;
+                p.max_depth = std::max(p.max_depth, st.max_depth);
+                p.kernel_ms += st.kernel_ms;
+                for (int k = 0; k < DASH_NUM_TIERS; k++) p.tier_systems[k] += st.tier_systems[k];
+                p.wave_rounds += st.wave_rounds;
             }
-            dash_stats& p = part[i];
-            for (int k = 0; k < DASH_NUM_TXN; k++) p.hist[k] += st.hist[k];
-            p.instructions += st.instructions;
-            p.rounds_total += st.rounds_total;
-            p.rounds_max = std::max(p.rounds_max, st.rounds_max);
-            p.systems += st.systems;
-            p.err_systems += st.err_systems;
-            p.err_bits |= st.err_bits;
-            p.dropped += st.dropped;
-            p.max_depth = std::max(p.max_depth, st.max_depth);
-            p.kernel_ms += st.kernel_ms;
-            for (int k = 0; k < DASH_NUM_TIERS; k++) p.tier_systems[k] += st.tier_systems[k];
-            p.wave_rounds += st.wave_rounds;
-        }
-    };
-    if (rc == DASH_OK) {
-        std::vector<std::thread> pool;
-        for (unsigned i = 0; i < nh; i++) {
-            try {
-                pool.emplace_back(lane, i);
-            } catch (...) {  // no thread: this lane's batches run on the calling thread
-                lane(i);
+        };
+        if (rc == DASH_OK) {
+            std::vector<std::thread> pool;
+            for (unsigned i = 0; i < nh; i++) {
+                try {
+                    pool.emplace_back(lane, i);
+                } catch (...) {  // no thread: this lane's batches run on the calling thread
+                    lane(i);
+                }
             }
+            for (auto& t : pool) t.join();
+            rc = trc[0] != DASH_OK ? trc[0] : trc[1];
+            if (rc != DASH_OK) set_global_msg(h[trc[0] != DASH_OK ? 0 : 1]->msg);
         }
-        for (auto& t : pool) t.join();
-        rc = trc[0] != DASH_OK ? trc[0] : trc[1];
-        if (rc != DASH_OK) set_global_msg(h[trc[0] != DASH_OK ? 0 : 1]->msg);
-    }
-    for (unsigned i = 0; i < nh; i++)
-        if (h[i]) dash_destroy(h[i]);
-    if (rc != DASH_OK) return rc;
-    *stats = part[0];
-    if (nh == 2) {
-        const dash_stats& q = part[1];
-        for (int k = 0; k < DASH_NUM_TXN; k++) stats->hist[k] += q.hist[k];
-        stats->instructions += q.instructions;
-        stats->rounds_total += q.rounds_total;
-        stats->rounds_max = std::max(stats->rounds_max, q.rounds_max);
-        stats->systems += q.systems;
-        stats->err_systems += q.err_systems;
-        stats->err_bits |= q.err_bits;
-        stats->dropped += q.dropped;
-        stats->max_depth = std::max(stats->max_depth, q.max_depth);
-        stats->kernel_ms += q.kernel_ms;
-        for (int k = 0; k < DASH_NUM_TIERS; k++) stats->tier_systems[k] += q.tier_systems[k];
-        stats->wave_rounds += q.wave_rounds;
-    }
-    return DASH_OK;
+        for (unsigned i = 0; i < nh; i++)
+            if (h[i]) dash_destroy(h[i]);
+        if (rc != DASH_OK) return rc;
+        *stats = part[0];
+        if (nh == 2) {
+            const dash_stats& q = part[1];
+            for (int k = 0; k < DASH_NUM_TXN; k++) stats->hist[k] += q.hist[k];
+            stats->instructions += q.instructions;
+            stats->rounds_total += q.rounds_total;
+            stats->rounds_max = std::max(stats->rounds_max, q.rounds_max);
+            stats->systems += q.systems;
+            stats->err_systems += q.err_systems;
+            stats->err_bits |= q.err_bits;
+            stats->dropped += q.dropped;
+            stats->max_depth = std::max(stats->max_depth, q.max_depth);
+            stats->kernel_ms += q.kernel_ms;
+            for (int k = 0; k < DASH_NUM_TIERS; k++) stats->tier_systems[k] += q.tier_systems[k];
+            stats->wave_rounds += q.wave_rounds;
+        }
+        return DASH_OK;
+    });
 }

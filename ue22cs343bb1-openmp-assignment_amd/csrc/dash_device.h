@@ -93,5 +93,9 @@ hipError_t launch_arb_table(uint64_t seed, uint32_t seg, uint32_t* out, uint32_t
 // RD words carry value 0 (ref :839): clears bits 7..0 of every word whose bit 15 is 0
 hipError_t launch_clear_rd(uint2* trace, uint64_t words, hipStream_t s);
 hipError_t launch_mark(const uint32_t* list, uint64_t n, uint8_t* skip, hipStream_t s);
+// box probe: blocks x 256 threads, 8 full-rate VALU per trip; clk[2 * block] = shader cycles,
+// clk[2 * block + 1] = 100-MHz reference ticks of that block's loop
+constexpr uint32_t PROBE_VALU_PER_TRIP = 8;
+hipError_t launch_probe(uint32_t blocks, uint32_t iters, uint32_t* sink, unsigned long long* clk, hipStream_t s);
 
 }  // namespace dash

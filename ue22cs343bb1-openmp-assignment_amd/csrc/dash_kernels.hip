@@ -120,6 +120,9 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
     static constexpr uint32_t WORDS = WND + WIN * WCHUNK * 64 / 2;
+    // the event-log kernel (MODE 2) only: this trip's events, u32 [64 lanes][4 slots][2]
+    static constexpr uint32_t EVS = WORDS;
+    static constexpr uint32_t EVS_WORDS = 64 * 4 * 2;
 };
 
 __device__ __forceinline__ void chunk_words(uint2 v, uint32_t& x, uint32_t& y) { x = v.x; y = v.y; }
@@ -180,7 +183,7 @@ void sim_kernel(const SimArgs a) {
     const uint32_t ncs = CS ? (uint32_t)CS : a.cache_size;  // cache lines per node
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS + (MODE == 2 ? L::EVS_WORDS : 0u)];
     uint16_t* const lds16 = reinterpret_cast<uint16_t*>(lds);
 
     const uint32_t lane = threadIdx.x;
@@ -267,6 +270,7 @@ void sim_kernel(const SimArgs a) {
     uint32_t err = 0, maxd = 0, drops = 0;  // maxd in ring-slot bytes until the end
     uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
     uint32_t nev = 0;         // events logged (DEBUG_MSG / DEBUG_INSTR emission, off unless a.events)
+    uint32_t nb = 0;          // of which staged in LDS this trip, not yet written (MODE 2)
     // loop-invariant uniform values a round needs, kept in VGPRs: the round's lane masks
     // need the SGPRs (spilling them costs VALU)
     // rcv_all: the nodes a REPLY_ID fan-out reaches (every node of the system but this one:
@@ -405,14 +409,12 @@ void sim_kernel(const SimArgs a) {
         // the popped message's type, or 13 (no transactionType) for a lane that does not pop:
         // the type masks below then need no AND with mHas
         const uint32_t pty = B(mHas) ? mty : 13u;
-        if (MODE == 2) {  // the batch-of-1 trace: the batch-of-1 trace (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652)
+        if (MODE == 2) {  // the event log (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652): staged in LDS
             COLD();
             if (B(mHas | mDo)) {
-                if (nev < a.event_cap) {
-                    uint32_t* e = a.events + ((sys * N + t) * a.event_cap + nev) * 2;
-                    e[0] = (rv + k) | (B(mHas) ? 0u : 0x80000000u);  // bit 31: an issued instruction
-                    e[1] = B(mHas) ? m : ins;
-                }
+                uint2* const es = reinterpret_cast<uint2*>(ldsb + L::EVS * 4) + lane * 4 + nb;
+                *es = make_uint2((rv + k) | (B(mHas) ? 0u : 0x80000000u), B(mHas) ? m : ins);  // bit 31: issued
+                ++nb;
                 ++nev;
             }
         }
@@ -648,6 +650,27 @@ void sim_kernel(const SimArgs a) {
         }
     };
 
+    // MODE 2: write the trip's staged events (at most one per round, so <= 4 per node) to the
+    // nodes' logs. Each node's events of a trip are contiguous in its log (positions nev - nb ..
+    // nev - 1); four lanes write one node's four 8-B slots, so one store instruction covers 16
+    // nodes' 32-B runs (16 lines) instead of 64 lanes' 8 B in 64 lines per round.
+    auto flush_events = [&]() __attribute__((always_inline)) {
+        asm volatile("" ::: "memory");  // the staging writes before the cross-lane reads
+        const uint32_t first = nev - nb;
+        const uint64_t lbase = (sys * N + t) * (uint64_t)a.event_cap;
+        const uint2* const es = reinterpret_cast<const uint2*>(ldsb + L::EVS * 4);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t n = q * 16 + (lane >> 2), slot = lane & 3u;
+            const uint32_t nbn = __shfl(nb, (int)n), fn = __shfl(first, (int)n);
+            const uint64_t lb = __shfl(lbase, (int)n);
+            if (slot < nbn && fn + slot < a.event_cap)
+                *reinterpret_cast<uint2*>(a.events + (lb + fn + slot) * 2) = es[n * 4 + slot];
+        }
+        asm volatile("" ::: "memory");
+        nb = 0;
+    };
+
     // TRIP rounds per trip of WCHUNK-round blocks, unrolled; the trip's start is the
     // housekeeping point (quiescence vote, overflow stop), each block's start the round-cap
     // test and the trace window refill
@@ -700,6 +723,7 @@ void sim_kernel(const SimArgs a) {
 #pragma unroll
             for (uint32_t k = WCHUNK + 1; k < TRIP; ++k) step(k, can_pop(), can_issue());
         }
+        if constexpr (MODE == 2) flush_events();
         rv += TRIP;
         mMsg = can_pop();
         mIss = can_issue();
@@ -934,6 +958,32 @@ hipError_t launch_mark(const uint32_t* list, uint64_t n, uint8_t* skip, hipStrea
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 1024);
     hipLaunchKernelGGL(mark_kernel, dim3(blocks), dim3(256), 0, s, list, n, skip);
+    return hipGetLastError();
+}
+
+// ---- box probe (dash_probe_box): a fixed VALU workload and the shader clock it ran at ----
+// Eight add/xor chains per lane (full-rate VOP2 ops) for `iters` trips; each workgroup's first
+// lane reads the shader-clock counter (s_memtime) and the constant 100-MHz counter
+// (s_memrealtime) around its loop, so cycles / reference ticks give the clock the box held.
+__global__ __launch_bounds__(256) void probe_kernel(uint32_t iters, uint32_t* sink, unsigned long long* clk) {
+    const uint64_t c0 = __builtin_amdgcn_s_memtime();
+    const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t a = threadIdx.x, b = a ^ 0x9E37u, c = a + 7u, d = a * 3u, e = a ^ 0x55u, f = a + 0x1234u,
+             g = a ^ 0xF0F0u, h = a + 99u;
+    for (uint32_t i = 0; i < iters; ++i) {
+        a += b; b ^= c; c += d; d ^= e; e += f; f ^= g; g += h; h ^= a;
+    }
+    const uint64_t c1 = __builtin_amdgcn_s_memtime();
+    const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+    if ((a ^ b ^ c ^ d ^ e ^ f ^ g ^ h) == 0x9E3779B9u) sink[0] = a;  // keeps the chains live
+    if (threadIdx.x == 0) {
+        clk[blockIdx.x * 2] = c1 - c0;
+        clk[blockIdx.x * 2 + 1] = r1 - r0;
+    }
+}
+
+hipError_t launch_probe(uint32_t blocks, uint32_t iters, uint32_t* sink, unsigned long long* clk, hipStream_t s) {
+    hipLaunchKernelGGL(probe_kernel, dim3(blocks), dim3(256), 0, s, iters, sink, clk);
     return hipGetLastError();
 }
 

@@ -52,7 +52,7 @@ EXPORTS = ("dash_create", "dash_destroy", "dash_last_error", "dash_load_traces",
            "dash_parse_core_file", "dash_resolve_dir", "dash_load_dir", "dash_init_node_state",
            "dash_dump_node", "dash_dump_file", "dash_digest_node", "dash_simulate_dir",
            "dash_read_events", "dash_format_event", "dash_load_dirs", "dash_dump_system",
-           "dash_write_digests", "dash_run_host_batched", "dash_set_schedule")
+           "dash_write_digests", "dash_run_host_batched", "dash_set_schedule", "dash_probe_box")
 SIT_OUT = 0xFF
 
 
@@ -100,6 +100,15 @@ class Stats(ctypes.Structure):
                 "wave_rounds": int(self.wave_rounds)}
 
 
+class BoxProbe(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 64), ("arch", ctypes.c_char * 32), ("compute_units", ctypes.c_int32),
+                ("clock_khz", ctypes.c_int32), ("mem_clock_khz", ctypes.c_int32), ("pci_domain", ctypes.c_int32),
+                ("pci_bus", ctypes.c_int32), ("pci_device", ctypes.c_int32), ("total_mem", ctypes.c_uint64),
+                ("probe_ms", ctypes.c_double), ("probe_valu_per_s", ctypes.c_double),
+                ("probe_sclk_mhz", ctypes.c_double), ("probe_sclk_min_mhz", ctypes.c_double),
+                ("probe_sclk_max_mhz", ctypes.c_double)]
+
+
 class Gen(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("sys_base", ctypes.c_uint64), ("kind", ctypes.c_uint32),
                 ("locality", ctypes.c_uint32), ("len", ctypes.c_uint32), ("_reserved", ctypes.c_uint32)]
@@ -128,6 +137,7 @@ def lib() -> ctypes.CDLL:
         "dash_load_traces": (i32, [vp, vp, u64, vp, u64]),
         "dash_generate": (i32, [vp, ctypes.POINTER(Gen)]),
         "dash_set_schedule": (i32, [vp, vp, u32]),
+        "dash_probe_box": (i32, [i32, ctypes.POINTER(BoxProbe)]),
         "dash_run": (i32, [vp, ctypes.POINTER(Stats)]),
         "dash_read_state": (i32, [vp, u64, ctypes.POINTER(NodeState)]),
         "dash_read_results": (i32, [vp, u64, u64, vp, vp, vp]),
@@ -159,7 +169,7 @@ def lib() -> ctypes.CDLL:
 
 
 # handle-less entry points whose failure text dash_last_error(NULL) holds (dash.h)
-_GLOBAL_MSG = ("dash_create", "dash_run_host_batched", "dash_simulate_dir")
+_GLOBAL_MSG = ("dash_create", "dash_run_host_batched", "dash_simulate_dir", "dash_probe_box")
 
 
 def _check(rc: int, what: str, handle=None):
@@ -212,6 +222,16 @@ def format_events(events, kinds=(0, 1)) -> str:
             _check(n if n < 0 else OK, "dash_format_event")
             out.append(buf.value.decode())
     return "".join(out)
+
+
+def probe_box(device=0) -> dict:
+    """dash_probe_box: device identity and clock limits, and a fixed VALU probe with the shader
+    clock the box held while it ran (a benchmark line's box description)."""
+    b = BoxProbe()
+    _check(lib().dash_probe_box(device, ctypes.byref(b)), "dash_probe_box")
+    d = {f: getattr(b, f) for f, _ in BoxProbe._fields_}
+    d["name"], d["arch"] = b.name.decode(errors="replace"), b.arch.decode(errors="replace")
+    return d
 
 
 def simulate_dir(test_dir, out_dir=".", num_procs=4, cache_size=4, max_instr=32, device=0) -> dict:

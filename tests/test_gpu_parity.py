@@ -441,6 +441,21 @@ def test_engine_reproduces_every_accepted_run(dash, name, tmp_path):
         assert dash.format_events(eng.read_events(0)) == log
 
 
+def test_cli_round_schedule_file(dash, tmp_path):
+    """`cache_simulator test_4 --rounds tests/golden/schedules/test_4_run_k.json`: the drop-in CLI
+    with an explicit round schedule writes each accepted run_k of test4.sh, byte-exact."""
+    exe = dash.PKG / "cache_simulator"
+    (tmp_path / "tests").mkdir()
+    shutil.copytree(GOLDEN / "test_4", tmp_path / "tests" / "test_4")
+    for run in ("run_1", "run_2", "run_3", "run_4"):
+        p = subprocess.run([str(exe), "test_4", "--rounds", str(SCHED_DIR / f"test_4_{run}.json")], cwd=tmp_path,
+                           capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        for n in range(4):
+            assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
+                (GOLDEN / "test_4" / run / f"core_{n}_output.txt").read_bytes(), (run, n)
+
+
 def test_set_schedule_checks_its_input(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32) as eng:

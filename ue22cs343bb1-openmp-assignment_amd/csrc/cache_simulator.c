@@ -14,6 +14,11 @@
  *       -D DEBUG_INSTR / -D DEBUG_MSG builds, README :104)
  *   --schedule SEED   a seeded legal schedule instead of lowest-sender-first (DESIGN.md §2;
  *       e.g. --schedule 87 lands tests/test_4 on its accepted run_2); also in bulk modes
+ *   --rounds FILE     an explicit round schedule (dash_set_schedule): one row per round, one
+ *       character per node, '-' = the node sits the round out, else its delivery position;
+ *       later rounds are lockstep. FILE is plain rows, or a JSON record of tests/golden/schedules
+ *       record (its "rounds" strings): e.g. tests/golden/schedules/test_4_run_3.json makes
+ *       `cache_simulator test_4` write the accepted run_3
  *
  * Bulk modes (one GPU batch, many systems; dumps go to OUT_DIR/<k>/):
  *   --batch LIST        system k = the k-th trace directory listed in LIST (one per line)
@@ -33,9 +38,56 @@ static const char *txn_names[DASH_NUM_TXN] = {
     "READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID", "INV", "UPGRADE",
     "WRITEBACK_INV", "WRITEBACK_INT", "FLUSH", "FLUSH_INVACK", "EVICT_SHARED", "EVICT_MODIFIED"};
 
-/* dash_simulate_dir plus a schedule seed and the event log of the one system */
+/* --rounds FILE: rows of n characters ('-' or a position digit); from a JSON record, the quoted
+   strings after its "rounds" key. Returns the row count, or -1 on a malformed file. */
+static long read_rounds(const char *path, unsigned n, uint8_t **out) {
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    static char text[1 << 20];
+    size_t len = fread(text, 1, sizeof text - 1, f);
+    fclose(f);
+    text[len] = 0;
+    const char *p = strstr(text, "\"rounds\"");
+    const int json = p != NULL;
+    if (!json) p = text;
+    else p += 8;
+    long rows = 0, cap = 0;
+    uint8_t *r = NULL;
+    while (*p) {
+        const char *q;
+        if (json) {  /* next quoted string, up to the array's end */
+            while (*p && *p != '"' && *p != ']') p++;
+            if (*p != '"') break;
+            q = ++p;
+            while (*p && *p != '"') p++;
+        } else {     /* next non-empty line */
+            while (*p == '\n' || *p == '\r' || *p == ' ') p++;
+            if (!*p) break;
+            q = p;
+            while (*p && *p != '\n' && *p != '\r' && *p != ' ') p++;
+        }
+        if ((unsigned)(p - q) != n) { free(r); return -1; }
+        if (rows == cap) {
+            cap = cap ? 2 * cap : 64;
+            r = (uint8_t *)realloc(r, (size_t)cap * n);
+        }
+        for (unsigned t = 0; t < n; t++) {
+            const char c = q[t];
+            if (c == '-') r[rows * n + t] = DASH_SIT_OUT;
+            else if (c >= '0' && c <= '7') r[rows * n + t] = (uint8_t)(c - '0');
+            else { free(r); return -1; }
+        }
+        rows++;
+        if (*p) p++;
+    }
+    *out = r;
+    return rows;
+}
+
+/* dash_simulate_dir plus a schedule (seed or explicit rounds) and the event log of the one system */
 static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m, const char *out, int dev,
-                           int dbg_instr, int dbg_msg, unsigned long long sched, dash_stats *st) {
+                           int dbg_instr, int dbg_msg, unsigned long long sched, const uint8_t *rounds,
+                           long nrounds, dash_stats *st) {
     dash_cfg cfg = {0};
     cfg.num_procs = n;
     cfg.cache_size = cs;
@@ -44,11 +96,12 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
     cfg.num_systems = 1;
     cfg.device = dev;
     cfg.trace_events = (dbg_instr || dbg_msg) ? 1u << 16 : 0;
-    cfg.schedule_seed = sched;
+    cfg.schedule_seed = rounds ? (sched ? sched : 1) : sched;
     dash_t *h = NULL;
     int rc = dash_create(&cfg, &h);
     if (rc != DASH_OK) return rc;
-    if ((rc = dash_load_dir(h, dir, 0)) == DASH_OK && (rc = dash_run(h, st)) == DASH_OK) {
+    if (rounds) rc = dash_set_schedule(h, rounds, (uint32_t)nrounds);
+    if (rc == DASH_OK && (rc = dash_load_dir(h, dir, 0)) == DASH_OK && (rc = dash_run(h, st)) == DASH_OK) {
         dash_node_state nodes[DASH_MAX_PROCS];
         rc = dash_read_state(h, 0, nodes);
         for (unsigned t = 0; rc == DASH_OK && t < n; t++) {
@@ -174,7 +227,7 @@ static int run_synthetic(uint64_t count, const bulk_opts *o) {
 int main(int argc, char *argv[]) {
     unsigned n = 4, cs = 4, m = 32;
     int dev = 0, show = 0, dbg_instr = 0, dbg_msg = 0, n_given = 0;
-    const char *out = ".", *dir = NULL, *batch = NULL, *digests = NULL, *dump = NULL;
+    const char *out = ".", *dir = NULL, *batch = NULL, *digests = NULL, *dump = NULL, *rounds_file = NULL;
     unsigned long long synth = 0, seed = 0x5EED, sched = 0;
     unsigned len = 4096, kind = DASH_GEN_UNIFORM;
     double loc = 0.5;
@@ -194,6 +247,7 @@ int main(int argc, char *argv[]) {
         else if (!strcmp(argv[i], "--len") && i + 1 < argc) len = (unsigned)atoi(argv[++i]);
         else if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = strtoull(argv[++i], NULL, 0);
         else if (!strcmp(argv[i], "--schedule") && i + 1 < argc) sched = strtoull(argv[++i], NULL, 0);
+        else if (!strcmp(argv[i], "--rounds") && i + 1 < argc) rounds_file = argv[++i];
         else if (!strcmp(argv[i], "--locality") && i + 1 < argc) loc = atof(argv[++i]);
         else if (!strcmp(argv[i], "--kind") && i + 1 < argc) {
             const char *k = argv[++i];
@@ -213,9 +267,17 @@ int main(int argc, char *argv[]) {
         fprintf(stderr, "Usage: %s <test_directory>\n", argv[0]); /* ref :128 */
         return EXIT_FAILURE;
     }
+    uint8_t *rounds = NULL;
+    long nrounds = 0;
+    if (rounds_file && (nrounds = read_rounds(rounds_file, n, &rounds)) < 0) {
+        fprintf(stderr, "cache_simulator: %s: not a round schedule for %u nodes\n", rounds_file, n);
+        return EXIT_FAILURE;
+    }
     dash_stats st;
-    int rc = (dbg_instr || dbg_msg || sched) ? simulate_traced(dir, n, cs, m, out, dev, dbg_instr, dbg_msg, sched, &st)
-                                             : dash_simulate_dir(dir, n, cs, m, out, dev, &st);
+    int rc = (dbg_instr || dbg_msg || sched || rounds_file)
+                 ? simulate_traced(dir, n, cs, m, out, dev, dbg_instr, dbg_msg, sched, rounds, nrounds, &st)
+                 : dash_simulate_dir(dir, n, cs, m, out, dev, &st);
+    free(rounds);
     if (rc != DASH_OK) {
         const char *why = dash_last_error(NULL);
         fprintf(stderr, "cache_simulator: %s (%d)\n", why[0] ? why : "failed", rc);

@@ -94,3 +94,14 @@ def test_ctypes_stub_reproduces_sample(tmp_path):
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr
     same_dumps(tmp_path)
+
+
+def test_schedule_snippet_compiles(tmp_path):
+    """The §2a snippet (an explicit round schedule through dash_set_schedule) compiles."""
+    body = blocks("c")[2]
+    assert "dash_set_schedule" in body
+    src = tmp_path / "sched.c"
+    src.write_text("#include <stdint.h>\n#include \"dash.h\"\nint main(void) {\n" + body +
+                   "    dash_destroy(h);\n    return (int)st.err_bits;\n}\n")
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", f"-I{ROOT / 'include'}", "-c", "-o",
+                    str(tmp_path / "sched.o"), str(src)], check=True, capture_output=True, text=True)

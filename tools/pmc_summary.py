@@ -68,5 +68,22 @@ if "SQ_ACTIVE_INST_VALU2" in agg and "SQ_CYCLES" in agg and "SQ_INSTS_VALU" in a
     res["valu_dual_issue_frac"] = agg["SQ_ACTIVE_INST_VALU2"] / q
 if "SQ_THREAD_CYCLES_VALU" in agg and "SQ_INSTS_VALU" in agg:
     res["valu_exec_lanes"] = agg["SQ_THREAD_CYCLES_VALU"] / agg["SQ_INSTS_VALU"]  # of 64
+# the box each pass ran on (bench.py's `box` object, round 4), from the pass's own line (DIR.log),
+# so a reader can compare the PMC box with the box of the bench line these counters annotate
+boxes = []
+for d in sys.argv[4:]:
+    log = pathlib.Path(d.rstrip("/") + ".log")
+    try:
+        line = json.loads([x for x in log.read_text().splitlines() if x.startswith("{")][-1])
+    except (OSError, IndexError, ValueError):
+        continue
+    b = line.get("box") or {}
+    pb, pa = b.get("probe_before") or {}, b.get("probe_after") or {}
+    boxes.append({"pass": pathlib.Path(d).name, "device": (b.get("device") or {}).get("name"),
+                  "pci_bus": (b.get("device") or {}).get("pci_bus"),
+                  "sclk_mhz": [pb.get("sclk_mhz"), pa.get("sclk_mhz")],
+                  "probe_ms": [pb.get("probe_ms"), pa.get("probe_ms")], "kernel_ms_avg": line.get("kernel_ms_avg")})
+if boxes:
+    res["boxes"] = boxes
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

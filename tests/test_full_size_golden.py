@@ -51,3 +51,30 @@ def test_round2_headline_line_matches_oracle(kind):
     assert tot["rounds_total"] == g["rounds_total"]
     assert tot["err_systems"] == g["err_systems"]
     assert tot["digest_sum"] == g["digest_sum"]
+
+
+SWEEP_GOLD = json.loads((ROOT / "tests" / "golden" / "sweep_full.json").read_text())
+
+
+def _sweep_points(path):
+    line = json.loads(path.read_text())
+    sw = line["sweep"]
+    return sw["points"] if isinstance(sw, dict) else sw
+
+
+@pytest.mark.parametrize("path", ["profiles/r03/final/sweep.json", "profiles/r04/bench_headline.json"])
+def test_committed_sweep_points_match_oracle_full_size(path):
+    """configs[4] at full size: three grid points of the committed GPU lines --
+    round 3's `bench.py --sweep` and round 4's default headline line, whose `sweep` object the
+    driver now times -- equal the oracle's run over all 2^20 systems (tests/golden/sweep_full.json,
+    make_sweep_full.py): histograms, instructions, rounds, error systems, digest checksum."""
+    f = ROOT / path
+    if not f.exists():
+        pytest.skip(f"{path} not committed yet")
+    assert SWEEP_GOLD["systems"] == 1 << 20 and SWEEP_GOLD["instr_per_node"] == 4096
+    pts = {(p["cache_size"], p["locality"]): p for p in _sweep_points(f)}
+    assert len(pts) == 25
+    for gp in SWEEP_GOLD["points"]:
+        p = pts[(gp["cache_size"], gp["locality"])]
+        for k in ("hist", "instructions", "rounds_total", "err_systems", "digest_sum"):
+            assert p[k] == gp[k], (path, gp["cache_size"], gp["locality"], k)

@@ -282,3 +282,30 @@ def test_seeded_schedules_are_strict_executions(test):
     for seed in range(1, 200):
         out, _ = oc.schedule_witness(tr, lens, arb_seed=seed)
         assert out.digest == oc.run_system(tr, lens, arb_seed=seed).digest
+
+
+def test_race_model_strands_messages():
+    """ORC_MICRO_RACE: the reference's unlocked count-- (:177) overwriting a concurrent count++
+    (:757) leaves an appended message uncounted, so its receiver stops draining with it inside.
+    On a two-node trace with one STRICT outcome, one such race yields new outcomes -- most of them
+    a requester waiting forever on a stranded reply (DEADLOCK) -- whose witnesses replay in the
+    RACE model and are rejected by the STRICT one."""
+    tr = np.zeros((2, 2), np.uint16)
+    tr[0] = [oc.pack("R", 0x10, 0), oc.pack("W", 0x11, 5)]
+    tr[1] = [oc.pack("W", 0x00, 7), oc.pack("R", 0x01, 0)]
+    lens = np.array([2, 2], np.uint32)
+    kw = dict(num_procs=2, cache_size=1)
+    strict, _, complete = oc.explore(tr, lens, micro=oc.MICRO_STRICT, max_states=100_000, **kw)
+    assert complete and len(strict) == 1 and strict[0].errors == 0
+    race = {}
+    for s in range(2000):
+        o, w = oc.random_walk(tr, lens, s + 1, micro=oc.MICRO_RACE, race_max=1, kind_weights=[1, 1, 1, 8], **kw)
+        race.setdefault(o.digest, (o, w))
+    new = [v for d, v in race.items() if d != strict[0].digest]
+    assert len(new) >= 5 and any(o.errors & oc.ERR_DEADLOCK for o, _ in new)
+    for o, w in new:
+        assert any(step >> 8 == 3 for step in w)  # each needed the race
+        r, terminal = oc.replay_steps(tr, lens, w, micro=oc.MICRO_RACE, race_max=1, **kw)
+        assert terminal and r.digest == o.digest
+        with pytest.raises(ValueError):
+            oc.replay_steps(tr, lens, w, micro=oc.MICRO_STRICT, **kw)

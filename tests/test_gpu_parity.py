@@ -58,10 +58,12 @@ def state_arrays(nodes, N, CS):
     return out
 
 
-def check_batch(dash, packed, lens, N, CS, max_rounds=0, flags=0, seed=0):
+def check_batch(dash, packed, lens, N, CS, max_rounds=0, flags=0, seed=0, sched=None):
     nsys = packed.shape[0]
     with dash.Engine(nsys, num_procs=N, cache_size=CS, max_instr=packed.shape[2], keep_state=True,
                      max_rounds=max_rounds, flags=flags, schedule_seed=seed) as eng:
+        if sched is not None:
+            eng.set_schedule(sched)
         eng.load_traces(packed, lens)
         stats = eng.run()
         dig, rnd, err = eng.read_results()
@@ -70,7 +72,8 @@ def check_batch(dash, packed, lens, N, CS, max_rounds=0, flags=0, seed=0):
         instr_total = 0
         for s in range(nsys):
             res = run_system(packed[s], lens[s], num_procs=N, cache_size=CS, ring_depth=256,
-                             max_rounds=max_rounds or (1024 + 256 * packed.shape[2]), arb_seed=seed)
+                             max_rounds=max_rounds or (1024 + 256 * packed.shape[2]), arb_seed=seed,
+                             sched=sched)
             gpu_nodes = eng.read_state(s)
             assert state_arrays(gpu_nodes, N, CS) == state_arrays(res.node, N, CS), f"system {s}"
             assert int(rnd[s]) == res.rounds, f"system {s} rounds"
@@ -454,6 +457,21 @@ def test_cli_round_schedule_file(dash, tmp_path):
         for n in range(4):
             assert (tmp_path / f"core_{n}_output.txt").read_bytes() == \
                 (GOLDEN / "test_4" / run / f"core_{n}_output.txt").read_bytes(), (run, n)
+
+
+@pytest.mark.parametrize("N,CS", [(8, 4), (5, 2), (4, 1)])
+def test_explicit_schedule_bit_exact(dash, N, CS):
+    """dash_set_schedule with random round tables (each node sits a round out with its own
+    probability, random delivery positions among all P lanes, 300 rounds, then lockstep):
+    every system bit-exact against the oracle's twin (orc_cfg.sched), contention included."""
+    rng = np.random.default_rng(1000 + N)
+    packed, lens = random_batch(rng, 96, N, 48, hot_frac=0.3)
+    P = 1 << (N - 1).bit_length()
+    R = 300
+    p = rng.uniform(0, 0.8, size=N)
+    pos = np.argsort(rng.random((R, P)), axis=1)[:, :N].astype(np.uint8)  # distinct, < P
+    sched = np.where(rng.random((R, N)) < p, dash.SIT_OUT, pos).astype(np.uint8)
+    check_batch(dash, packed, lens, N, CS, seed=1, sched=sched)
 
 
 def test_set_schedule_checks_its_input(dash):

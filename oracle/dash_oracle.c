@@ -1509,3 +1509,212 @@ done:
     free(c.scratch);
     return rc;
 }
+
+/* ==== engine round schedules from the reference's own logs (round 4) ====
+ *
+ * orc_rounds_from_logs searches the ENGINE's round model -- each round, a chosen set of nodes
+ * each takes one step on start-of-round state (pop if its queue is non-empty, else issue), then
+ * the round's messages are appended sender by sender in a chosen order -- for a schedule under
+ * which every node pops exactly the messages of its reference log, in order, and issues where
+ * the log says. The resulting table is a dash_set_schedule input: the GPU engine then re-enacts
+ * that reference run, and its own DEBUG event log must equal the reference's, thread by thread.
+ * A round is built from the optional nodes (a queued head that is the node's next logged pop, or
+ * an issue its log expects next); nodes whose log waits for a message sit out. The messages in a
+ * queue must always be a prefix of the node's upcoming run of logged pops (a message arriving
+ * before the node's logged issue would be popped first), which fixes, per receiver, the order of
+ * the round's senders; the senders are then ordered by those precedences. Subsets of the
+ * optional nodes are tried largest first (depth-first, visited states hashed). */
+
+typedef struct {
+    xsys s;
+    uint32_t depth;
+    uint8_t row[ORC_MAX_PROCS];
+} xrent;
+
+/* round with stepping set `mask` from state *s; on success writes the delivery row and returns
+   1 (*s advanced), else 0 */
+static int r_try(xctx *c, const xguide *g, xsys *s, uint32_t mask, uint8_t *row) {
+    for (int t = 0; t < c->N; t++) {
+        if (!((mask >> t) & 1)) continue;
+        if (s->n[t].qn > 0) x_pop(c, s, t);
+        else x_step(c, s, t, NULL);
+    }
+    /* precedences among senders: prec[a] has bit b when a must deliver before b */
+    uint32_t prec[ORC_MAX_PROCS] = {0};
+    for (int r = 0; r < c->N; r++) {
+        const xnode *x = &s->n[r];
+        const int k0 = g_cursor(s, r);
+        /* the queue, then this round's arrivals, must follow r's upcoming run of logged pops */
+        int run = 0;
+        while ((uint32_t)(k0 + run) < g->n[r] && !(g->ev[r][k0 + run] >> 31)) run++;
+        int pos = x->qn;
+        if (pos > run) return 0;
+        for (int i = 0; i < x->qn; i++) {
+            const uint32_t e = g->ev[r][k0 + i];
+            if ((e & 0xFF) != x->q[i].type || ((e >> 8) & 0xFF) != x->q[i].sender ||
+                ((e >> 16) & 0xFF) != x->q[i].address)
+                return 0;
+        }
+        /* each sender's block to r, in program order: match it at the position its first
+           message has in the run */
+        int placed = 0, last = -1;
+        uint32_t done = 0;
+        for (;;) {
+            int total = 0;
+            for (int snd = 0; snd < c->N; snd++)
+                if (!((done >> snd) & 1))
+                    for (int k = 0; k < s->n[snd].on; k++) total += s->n[snd].oto[k] == r;
+            if (total == 0) break;
+            if (pos >= run) return 0;  /* more arrivals than logged pops before r's next issue */
+            const uint32_t e = g->ev[r][k0 + pos];
+            const int snd = (int)((e >> 8) & 0xFF);
+            if (snd >= c->N || ((done >> snd) & 1)) return 0;
+            const xnode *sx = &s->n[snd];
+            int n_to = 0;
+            for (int k = 0; k < sx->on; k++) {
+                if (sx->oto[k] != r) continue;
+                if (pos + n_to >= run) return 0;
+                const uint32_t f = g->ev[r][k0 + pos + n_to];
+                if ((f & 0xFF) != sx->o[k].type || ((f >> 8) & 0xFF) != sx->o[k].sender ||
+                    ((f >> 16) & 0xFF) != sx->o[k].address)
+                    return 0;
+                n_to++;
+            }
+            if (n_to == 0) return 0;  /* the logged next sender sent r nothing this round */
+            pos += n_to;
+            done |= 1u << snd;
+            if (last >= 0) prec[last] |= 1u << snd;
+            last = snd;
+            placed++;
+        }
+        (void)placed;
+    }
+    /* a delivery order honouring the precedences (Kahn), stepping senders first by id */
+    uint32_t left = (1u << c->N) - 1, p = 0;
+    uint8_t order[ORC_MAX_PROCS];
+    while (left) {
+        int pick = -1;
+        for (int a = 0; a < c->N && pick < 0; a++) {
+            if (!((left >> a) & 1)) continue;
+            int blocked = 0;
+            for (int b = 0; b < c->N; b++)
+                if (((left >> b) & 1) && ((prec[b] >> a) & 1)) blocked = 1;
+            if (!blocked) pick = a;
+        }
+        if (pick < 0) return 0;  /* contradictory orders across receivers */
+        order[p++] = (uint8_t)pick;
+        left &= ~(1u << pick);
+    }
+    for (int k = 0; k < c->N; k++) {
+        const int snd = order[k];
+        while (s->n[snd].on > 0) x_send(c, s, snd);
+    }
+    for (int t = 0; t < c->N; t++) row[t] = 0xFF;
+    for (int k = 0; k < c->N; k++)
+        if ((mask >> order[k]) & 1) row[order[k]] = (uint8_t)k;
+    /* positions must be distinct among stepping nodes only; the rest sit out */
+    return 1;
+}
+
+int orc_rounds_from_logs(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                         const uint32_t *events, const uint32_t *ev_count, uint64_t max_states,
+                         uint8_t *sched, uint32_t sched_cap, uint32_t *n_rounds, int *found, uint64_t *states) {
+    xctx c;
+    orc_cfg cf = *cfg;
+    cf.micro = ORC_MICRO_STRICT;
+    if (x_setup(&c, &cf, trace, stride, lens, 0)) return -1;
+    c.guided = 1;
+    xguide g;
+    uint64_t off = 0;
+    for (int t = 0; t < c.N; t++) {
+        g.ev[t] = events + off;
+        g.n[t] = ev_count[t];
+        off += ev_count[t];
+    }
+    xset vis;
+    vis.cap = 1;
+    while (vis.cap < max_states + max_states / 2 + 2) vis.cap <<= 1;
+    vis.keys = (uint64_t *)calloc(vis.cap, sizeof(uint64_t));
+    vis.n = 0;
+    size_t scap = 256, sn = 0, pcap = 1024;
+    xrent *stack = (xrent *)malloc(sizeof(xrent) * scap);
+    uint8_t *path = (uint8_t *)malloc((size_t)pcap * ORC_MAX_PROCS);
+    int rc = 0, hit = 0;
+    uint32_t hit_len = 0;
+    if (!vis.keys || !stack || !path) { rc = -1; goto done; }
+    x_init(&c, &stack[0].s);
+    stack[0].depth = 0;
+    sn = 1;
+    while (sn > 0 && !hit) {
+        const xrent e = stack[--sn];
+        if (e.depth > 0) {
+            if (e.depth > pcap) {
+                pcap *= 2;
+                uint8_t *np = (uint8_t *)realloc(path, (size_t)pcap * ORC_MAX_PROCS);
+                if (!np) { rc = -1; break; }
+                path = np;
+            }
+            memcpy(path + (size_t)(e.depth - 1) * ORC_MAX_PROCS, e.row, ORC_MAX_PROCS);
+        }
+        const xsys *s = &e.s;
+        /* optional nodes; dead if a queued head is not the node's next logged pop */
+        uint32_t opt = 0;
+        int dead = 0, finished = 1;
+        for (int t = 0; t < c.N && !dead; t++) {
+            const xnode *x = &s->n[t];
+            const int k = g_cursor(s, t);
+            const int more = (uint32_t)k < g.n[t];
+            if (more || x->qn) finished = 0;
+            if (x->qn > 0) {
+                if (!more || (g.ev[t][k] >> 31)) { dead = 1; break; }
+                opt |= 1u << t;  /* the head was checked when it arrived */
+            } else if (!x->waiting && x->idx < c.count[t]) {
+                if (!more) { dead = 1; break; }
+                if (g.ev[t][k] >> 31) opt |= 1u << t;
+            }
+        }
+        if (dead) continue;
+        if (finished) {
+            hit = 1;
+            hit_len = e.depth;
+            break;
+        }
+        /* subsets of opt, largest first; pushed in reverse so the largest is tried first */
+        uint32_t subs[256];
+        int ns = 0;
+        for (int bits = c.N; bits >= 1; bits--)
+            for (uint32_t m = opt; m; m = (m - 1) & opt)
+                if (__builtin_popcount(m) == bits) subs[ns++] = m;
+        for (int i = ns - 1; i >= 0; i--) {
+            xrent nx;
+            nx.s = *s;
+            if (!r_try(&c, &g, &nx.s, subs[i], nx.row)) continue;
+            if (vis.n >= max_states) continue;
+            if (!xset_insert(&vis, x_hash(&c, &nx.s))) continue;
+            nx.depth = e.depth + 1;
+            if (sn == scap) {
+                scap *= 2;
+                xrent *ns2 = (xrent *)realloc(stack, sizeof(xrent) * scap);
+                if (!ns2) { rc = -1; break; }
+                stack = ns2;
+            }
+            stack[sn++] = nx;
+        }
+        if (rc) break;
+    }
+    if (hit) {
+        if (hit_len > sched_cap) rc = -2;
+        else
+            for (uint32_t r = 0; r < hit_len; r++)
+                memcpy(sched + (size_t)r * c.N, path + (size_t)r * ORC_MAX_PROCS, (size_t)c.N);
+    }
+done:
+    if (found) *found = hit;
+    if (n_rounds) *n_rounds = hit ? hit_len : 0;
+    if (states) *states = vis.n;
+    free(vis.keys);
+    free(stack);
+    free(path);
+    free(c.scratch);
+    return rc;
+}

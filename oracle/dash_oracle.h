@@ -193,6 +193,14 @@ int orc_guided(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const
                const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
                orc_outcome *out, uint64_t *states, int *complete);
 
+/* An engine round schedule (dash_set_schedule form, [rounds][num_procs]) under which every node
+   pops exactly its logged messages and issues where its log says (events as for orc_guided).
+   *found = 0 when the search ends without one (the run is not a round-model execution, or the
+   state budget ran out). */
+int orc_rounds_from_logs(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                         const uint32_t *events, const uint32_t *ev_count, uint64_t max_states,
+                         uint8_t *sched, uint32_t sched_cap, uint32_t *n_rounds, int *found, uint64_t *states);
+
 #ifdef __cplusplus
 }
 #endif

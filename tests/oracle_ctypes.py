@@ -92,6 +92,8 @@ def bind(path):
     L.orc_replay_steps.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, I, V, ctypes.c_uint32, V, V]
     L.orc_guided.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, V, U64, V, V, V, V]
     L.orc_guided.restype = ctypes.c_int
+    L.orc_rounds_from_logs.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, V, U64, V, ctypes.c_uint32, V, V, V]
+    L.orc_rounds_from_logs.restype = ctypes.c_int
     L.orc_schedule_witness.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, ctypes.c_uint32, V, V]
     for f in (L.orc_replay_lockstep, L.orc_random_schedule, L.orc_explore, L.orc_reach,
               L.orc_random_walk, L.orc_replay_steps, L.orc_schedule_witness):
@@ -348,6 +350,22 @@ def guided(trace, lens, events, num_procs=4, cache_size=4, max_states=2_000_000,
     if rc != 0:
         raise ValueError(f"guided search failed ({rc})")
     return bool(found.value), out, int(states.value), bool(full.value)
+
+
+def rounds_from_logs(trace, lens, events, num_procs=4, cache_size=4, max_states=500_000, cap=4096):
+    """orc_rounds_from_logs: (engine round schedule uint8 [rounds][num_procs] or None, states)."""
+    trace, lens = _tr(trace, lens)
+    cfg = OrcCfg(num_procs, cache_size, 256, 0, 0, MICRO_STRICT, 0)
+    flat = np.ascontiguousarray([w for e in events for w in e] or [0], dtype=np.uint32)
+    cnt = np.ascontiguousarray([len(e) for e in events], dtype=np.uint32)
+    out = np.zeros((cap, num_procs), np.uint8)
+    nr, found, states = ctypes.c_uint32(), ctypes.c_int(), ctypes.c_uint64()
+    rc = lib().orc_rounds_from_logs(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1], lens.ctypes.data,
+                                    flat.ctypes.data, cnt.ctypes.data, max_states, out.ctypes.data, cap,
+                                    ctypes.addressof(nr), ctypes.addressof(found), ctypes.addressof(states))
+    if rc != 0:
+        raise ValueError(f"rounds_from_logs failed ({rc})")
+    return (out[:nr.value].copy() if found.value else None), int(states.value)
 
 
 def schedule_witness(trace, lens, num_procs=4, cache_size=4, arb_seed=0, sched=None,

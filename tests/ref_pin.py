@@ -362,6 +362,47 @@ def guided_mutant_kills(runs, n=4, max_states=2_000_000):
     return kills
 
 
+def replay_cases(n):
+    """tests/golden/ref_runs/replay{n}.json (make_ref_replays.py): reference runs with an engine
+    round schedule each. Yields (case, cache_size, trace, lens, schedule uint8 [rounds][n])."""
+    data = json.loads((oc.ROOT / "tests" / "golden" / "ref_runs" / f"replay{n}.json").read_text())
+    for c in data["cases"]:
+        rows = [[oc.pack(w[0][0], int(w[1], 16), int(w[2]) if len(w) > 2 else 0)
+                 for w in (ln.split() for ln in r)] for r in c["trace"]]
+        tr, lens = as_arrays(rows)
+        sched = np.array([[0xFF if ch == "-" else int(ch) for ch in row] for row in c["rounds"]],
+                         np.uint8).reshape(len(c["rounds"]), n)
+        yield c, c["cache_size"], tr, lens, sched
+
+
+def log_tokens(text, n):
+    """Each thread's DEBUG_MSG / DEBUG_INSTR lines (ref :179-182, :649-652) as tokens, in the
+    thread's order: pops "type.sender.ADDR", issues "R.ADDR" / "W.ADDR.value"."""
+    out = [[] for _ in range(n)]
+    for ln in text.splitlines():
+        m = oc.LOG_MSG.match(ln)
+        if m:
+            out[int(m[1])].append(f"{int(m[3])}.{int(m[2])}.{int(m[4], 16):02X}")
+            continue
+        m = oc.LOG_INSTR.match(ln)
+        if m:
+            a = int(m[3], 16)
+            out[int(m[1])].append(f"W.{a:02X}.{int(m[4])}" if m[2] == "W" else f"R.{a:02X}")
+    return [" ".join(t) for t in out]
+
+
+def event_tokens(kind_word_node, n):
+    """Per-node tokens of (node, is_instr, word) events, as make_ref_replays.py writes them."""
+    out = [[] for _ in range(n)]
+    for node, instr, w in kind_word_node:
+        a = (w >> 8) & 0x7F
+        if instr:
+            out[node].append(f"W.{a:02X}.{w & 0xFF}" if w & 0x8000 else f"R.{a:02X}")
+        else:
+            out[node].append(f"{w & 15}.{(w >> 4) & 7}.{a:02X}")
+    return [" ".join(t) for t in out]
+
+
 def explorer_reach(seeds, n, max_states=MAX_STATES):
     """How many of the guided pin's traces the complete explorer (round 3) could not finish."""
     skipped = 0

@@ -474,6 +474,29 @@ def test_explicit_schedule_bit_exact(dash, N, CS):
     check_batch(dash, packed, lens, N, CS, seed=1, sched=sched)
 
 
+@pytest.mark.parametrize("n", [4, 8])
+def test_engine_reenacts_reference_runs(dash, n):
+    """The GPU engine against the reference itself, not the oracle: 40 runs per node count of the
+    reference binary (tests/golden/ref_runs/, past complete exploration) whose own DEBUG logs
+    define an engine round schedule (make_ref_replays.py). Driven by that schedule through
+    dash_set_schedule, the engine's event log equals the reference's DEBUG_MSG / DEBUG_INSTR
+    lines thread by thread, and its final state is the reference's dumps (digest)."""
+    import ref_pin
+    k = 0
+    for c, cs, tr, lens, sched in ref_pin.replay_cases(n):
+        with dash.Engine(1, num_procs=n, cache_size=cs, max_instr=32, trace_events=512, schedule_seed=1) as eng:
+            eng.set_schedule(sched)
+            eng.load_traces(tr[None], lens[None])
+            eng.run()
+            dig = int(eng.read_results()[0][0])
+            ev = eng.read_events(0)
+        assert dig == int(c["digest"], 16), c["seed"]
+        got = ref_pin.event_tokens([(e.node, e.kind == dash.EV_INSTR, e.word) for e in ev], n)
+        assert got == c["log"], c["seed"]
+        k += 1
+    assert k == 40
+
+
 def test_set_schedule_checks_its_input(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32) as eng:

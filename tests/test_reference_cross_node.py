@@ -112,3 +112,19 @@ def test_logged_reference_runs_refute_every_mutant(n):
             assert (not f and complete) or [oc.dump_node(r, k, cs, L=L) for k in range(n)] != c["dumps"], (m, c["seed"])
             refuted.add(int(m[1:]))
     assert refuted == set(ref_pin.MUTANTS)
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_reference_runs_replay_on_the_round_model(n):
+    """Reference runs that are executions of the ENGINE's round model (tests/golden/ref_runs/,
+    make_ref_replays.py: 40 per node count, schedules derived from the runs' own logs by
+    orc_rounds_from_logs): the oracle's round runner under each schedule prints exactly the
+    reference's DEBUG_MSG / DEBUG_INSTR lines, thread by thread, and ends in its dumps (digest).
+    tests/test_gpu_parity.py holds the GPU engine to the same runs."""
+    k = 0
+    for c, cs, tr, lens, sched in ref_pin.replay_cases(n):
+        res, log = oc.run_system(tr, lens, num_procs=n, cache_size=cs, sched=sched, log=True, log_msgs=True)
+        assert res.digest == int(c["digest"], 16), c["seed"]
+        assert ref_pin.log_tokens(log, n) == c["log"], c["seed"]
+        k += 1
+    assert k == 40

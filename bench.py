@@ -234,6 +234,63 @@ def sysfs_gpu(pci_domain, pci_bus):
     return None
 
 
+class ClockSampler:
+    """Samples the GPU's current shader clock from sysfs (hwmon freq1_input, else the starred
+    pp_dpm_sclk level) every `period` s on a thread while the timed region runs (dash_run
+    releases the GIL), so a line shows whether the box held its clock under the sustained load."""
+
+    def __init__(self, sysfs_dev, period=0.05):
+        import glob
+        import threading
+        self.files = sorted(glob.glob(f"{sysfs_dev}/hwmon/hwmon*/freq1_input")) if sysfs_dev else []
+        self.dpm = f"{sysfs_dev}/pp_dpm_sclk" if sysfs_dev else None
+        self.period, self.samples, self.stop_ev = period, [], threading.Event()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _read(self):
+        try:
+            if self.files:
+                return int(pathlib.Path(self.files[0]).read_text()) / 1e6
+            for ln in pathlib.Path(self.dpm).read_text().splitlines():
+                if ln.strip().endswith("*"):
+                    return float(ln.split(":")[1].lower().replace("mhz", "").replace("*", "").strip())
+        except (OSError, ValueError, IndexError, TypeError):
+            return None
+        return None
+
+    def _run(self):
+        while not self.stop_ev.wait(self.period):
+            v = self._read()
+            if v is not None:
+                self.samples.append(v)
+
+    def __enter__(self):
+        if self.files or self.dpm:
+            self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop_ev.set()
+        if self.th.is_alive():
+            self.th.join()
+
+    def summary(self):
+        s = sorted(self.samples)
+        if not s:
+            return None
+        return {"n": len(s), "min_mhz": s[0], "median_mhz": s[len(s) // 2], "max_mhz": s[-1],
+                "source": "hwmon freq1_input" if self.files else "pp_dpm_sclk (starred level)"}
+
+
+def sysfs_dev_path(pci_domain, pci_bus):
+    import glob
+    want = f"{pci_domain:04x}:{pci_bus:02x}:"
+    for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+        if os.path.basename(os.path.realpath(dev)).lower().startswith(want):
+            return dev
+    return None
+
+
 def box_probe(dash, dev):
     """dash_probe_box (the device, its clock limits, a fixed VALU probe and the shader clock it
     ran at) plus the sysfs clock levels, sampled around the timed region."""
@@ -626,9 +683,10 @@ def vector_pipe(prof, wave_rounds):
             "(tools/micro/valu_ops), static mix from profiles/isa_table.json"}
 
 
-def run_kind(dash, args, kind_name, M, sys_base, world, dev, steps, tier_flag):
-    """One workload (uniform / contention / locality): generate on the device, time it,
-    all-reduce the totals; returns (elapsed, totals, stats, kernel_ms)."""
+def run_kind(dash, args, kind_name, M, sys_base, world, dev, steps, tier_flag, sampler=None):
+    """One workload (uniform / contention / locality): generate on the device, time it (the
+    optional ClockSampler samples the clock meanwhile), all-reduce the totals; returns
+    (elapsed, totals, stats, kernel_ms)."""
     import torch
     kind = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
             "locality": dash.GEN_LOCALITY}[kind_name]
@@ -639,7 +697,11 @@ def run_kind(dash, args, kind_name, M, sys_base, world, dev, steps, tier_flag):
         eng.generate(args.seed, args.len, kind=kind, locality=locality, sys_base=sys_base)
         a = argparse.Namespace(**vars(args))
         a.steps = steps
-        elapsed, stats, kernel_ms = timed_headline(eng, a, world, dev)
+        if sampler is not None:
+            with sampler:
+                elapsed, stats, kernel_ms = timed_headline(eng, a, world, dev)
+        else:
+            elapsed, stats, kernel_ms = timed_headline(eng, a, world, dev)
         # a checksum of the per-system state digests (sums of their 32-bit
         # halves: order-free, so identical for any GPU count), read back after the timed region
         dsum = digest_sum(eng.read_results()[0])
@@ -803,8 +865,10 @@ def main():
     tier_flag = {0: 0, 32: dash.TIER_FROM_32, 256: dash.TIER_FROM_256}[args.first_depth]
     sys_base, M = shard(rank, world, args.systems)
     probe0 = box_probe(dash, dev)
+    pdev = probe0.get("_dev") or {}
+    sampler = ClockSampler(sysfs_dev_path(pdev["pci_domain"], pdev["pci_bus"])) if pdev else None
     elapsed, totals, stats, kernel_ms = run_kind(dash, args, args.kind, M, sys_base, world, dev,
-                                                 args.steps, tier_flag)
+                                                 args.steps, tier_flag, sampler)
     probe1 = box_probe(dash, dev)
     instr_per_step = world * M * 8 * args.len
     value = instr_per_step * args.steps / elapsed
@@ -915,7 +979,8 @@ def main():
                             "semantics under the lockstep schedule"),
             "contention": cont,
             "sweep": sweep_obj,
-            "box": box_record(probe0, probe1),
+            "box": dict(box_record(probe0, probe1),
+                        sclk_during_timed_steps=sampler.summary() if sampler else None),
         }
         print(json.dumps(line), flush=True)
 

@@ -7,8 +7,10 @@
 set -uo pipefail
 TAG=$1; OUT=gpurun_out/ev_$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
-step bench "(the driver's command)"
-timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
+if [ -z "${SKIP_BENCH:-}" ]; then
+  step bench "(the driver's command)"
+  timeout -k 10 500 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 1
+fi
 step kernel trace, uniform launches only
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_uniform" -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --contention-steps 0 --line-sweep off > "$OUT/trace_uniform.log" 2>&1 || exit 1

@@ -764,6 +764,9 @@ def main():
                     help="the configs[4] grid inside the headline line (`sweep` object): auto = only with the "
                          "full-size uniform headline workload")
     ap.add_argument("--line-sweep-steps", type=int, default=1, help="timed steps per sweep point in the line")
+    ap.add_argument("--line-next", choices=["auto", "on", "off"], default="auto",
+                    help="the DEBUG event-log and seeded-schedule rows of --next inside the headline line (`next` "
+                         "object): auto = only with the full-size uniform headline on one GPU")
     ap.add_argument("--line-sweep-warmup", type=int, default=1, help="untimed steps per sweep point in the line")
     ap.add_argument("--cpu-kind", choices=["port", "reference"], default="reference",
                     help="headline cpu_baseline: the reference binary itself (oracle/_ref/cache_simulator_bench, "
@@ -901,6 +904,15 @@ def main():
     line_sweep = args.line_sweep == "on" or (args.line_sweep == "auto" and full and args.kind == "uniform")
     points = sweep_gpu(args, dash, rank, world, dev, args.line_sweep_steps, args.line_sweep_warmup) \
         if line_sweep else None
+    # two SURVEY §8(f) rows beside the hot path, driver-observed on one GPU (bench_next.py): the
+    # DEBUG event log against the fast kernel, and the seeded legal schedules at the headline size
+    line_next = args.line_next == "on" or (args.line_next == "auto" and full and args.kind == "uniform"
+                                           and world == 1)
+    next_rows = None
+    if line_next:
+        import bench_next
+        next_rows = {"events": bench_next.events_row(dash, dev, args.seed, args.next_event_systems, args.len),
+                     "seeded": bench_next.seeded_row(dash, dev, args.seed, M, args.len, 1)}
 
     # the CPU legs run after the timed regions and after the process group is gone, on rank 0
     # only, for every --gpus N (the ratio north_star states is the 8-GPU one)
@@ -979,6 +991,7 @@ def main():
                             "semantics under the lockstep schedule"),
             "contention": cont,
             "sweep": sweep_obj,
+            "next": next_rows,
             "box": dict(box_record(probe0, probe1),
                         sclk_during_timed_steps=sampler.summary() if sampler else None),
         }

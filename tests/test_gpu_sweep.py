@@ -57,7 +57,7 @@ def test_headline_line_carries_the_sweep():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--systems", str(GOLD["systems"]),
                         "--len", str(GOLD["instr_per_node"]), "--seed", str(GOLD["seed"]), "--steps", "1",
                         "--warmup", "0", "--contention-steps", "0", "--line-sweep", "on", "--cpu-seconds", "0.2",
-                        "--ref-instances", "2"],
+                        "--ref-instances", "2", "--line-next", "on", "--next-event-systems", "256"],
                        capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
@@ -78,6 +78,9 @@ def test_headline_line_carries_the_sweep():
         assert pb["probe_ms"] > 0 and 300 < pb["sclk_mhz"] <= box["device"]["clock_khz"] / 1e3 * 1.05, pb
     cb = line["cpu_baseline"]["batches"]
     assert cb["min"] <= cb["median"] <= cb["max"]
+    nx = line["next"]  # the event-log and seeded-schedule rows, each with its parity property
+    assert nx["events"]["parity_same_digests_as_fast"] and nx["events"]["parity_events_logged"]
+    assert nx["seeded"]["parity_all_issued"] and nx["seeded"]["parity_reproducible"]
 
 
 FULL = ROOT / "tests" / "golden" / "sweep_full.json"

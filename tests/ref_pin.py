@@ -210,7 +210,10 @@ def run(count=COUNT, runs=RUNS, max_states=MAX_STATES, n=4):
     def explore(seed):
         cs, rows = gen_trace(seed, n)
         tr, lens = as_arrays(rows)
-        outs, _, complete = oc.explore(tr, lens, num_procs=n, cache_size=cs, max_states=max_states)
+        # the STRICT model (round 4): a thread's sends complete before its next step, exactly the
+        # race-free reference; its complete sets are subsets of the round-3 BUFFERED ones
+        outs, _, complete = oc.explore(tr, lens, num_procs=n, cache_size=cs, max_states=max_states,
+                                       micro=oc.MICRO_STRICT)
         legal = {tuple(oc.dump_node(o, k, cs) for k in range(n)) for o in outs} if complete else None
         return seed, cs, rows, legal
 
@@ -264,7 +267,8 @@ def mutant_kills(cases, max_states=MAX_STATES, n=4):
         def killed(case):
             seed, cs, rows, seen = case
             tr, lens = as_arrays(rows)
-            outs, _, complete = oc.explore(tr, lens, num_procs=n, cache_size=cs, max_states=max_states, L=L)
+            outs, _, complete = oc.explore(tr, lens, num_procs=n, cache_size=cs, max_states=max_states, L=L,
+                                           micro=oc.MICRO_STRICT)
             if not complete:
                 return False
             legal = {tuple(oc.dump_node(o, k, cs, L=L) for k in range(n)) for o in outs}

@@ -24,7 +24,8 @@ def complete_cases():
     def one(seed):
         cs, rows = ref_pin.gen_trace(seed, N)
         tr, lens = ref_pin.as_arrays(rows)
-        outs, _, complete = oc.explore(tr, lens, num_procs=N, cache_size=cs, max_states=ref_pin.MAX_STATES)
+        outs, _, complete = oc.explore(tr, lens, num_procs=N, cache_size=cs, max_states=ref_pin.MAX_STATES,
+                                       micro=oc.MICRO_STRICT)
         legal = {tuple(oc.dump_node(o, k, cs) for k in range(N)) for o in outs} if complete else None
         return cs, tr, lens, legal
     with ThreadPoolExecutor(8) as pool:

@@ -120,8 +120,9 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
     static constexpr uint32_t WORDS = WND + WIN * WCHUNK * 64 / 2;
-    // the event-log kernel (MODE 2) only: this trip's events, u32 [64 lanes][4 slots][2]
-    static constexpr uint32_t EVS = WORDS;
+    // the event-log kernel (MODE 2) only: this trip's events, u32 [64 lanes][4 slots][2], 16-B
+    // aligned (WORDS is odd for some instantiations; the staging accesses are 8-B ds ops)
+    static constexpr uint32_t EVS = (WORDS + 3u) & ~3u;
     static constexpr uint32_t EVS_WORDS = 64 * 4 * 2;
 };
 
@@ -183,7 +184,7 @@ void sim_kernel(const SimArgs a) {
     const uint32_t ncs = CS ? (uint32_t)CS : a.cache_size;  // cache lines per node
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS + (MODE == 2 ? L::EVS_WORDS : 0u)];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[MODE == 2 ? L::EVS + L::EVS_WORDS : L::WORDS];
     uint16_t* const lds16 = reinterpret_cast<uint16_t*>(lds);
 
     const uint32_t lane = threadIdx.x;

@@ -13,12 +13,12 @@ if [ -z "${SKIP_BENCH:-}" ]; then
 fi
 step kernel trace, uniform launches only
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_uniform" -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --contention-steps 0 --line-sweep off > "$OUT/trace_uniform.log" 2>&1 || exit 1
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --contention-steps 0 --line-sweep off --line-next off > "$OUT/trace_uniform.log" 2>&1 || exit 1
 pmc() {  # kind name counters...
   local kind=$1 name=$2; shift 2
   step pmc "$kind" "$name"
   timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$OUT/pmc_$kind/$name" -o run -- \
-      python3 bench.py --kind "$kind" --steps 1 --warmup 0 --no-cpu-baseline --contention-steps 0 --line-sweep off \
+      python3 bench.py --kind "$kind" --steps 1 --warmup 0 --no-cpu-baseline --contention-steps 0 --line-sweep off --line-next off \
       > "$OUT/pmc_$kind/$name.log" 2>&1 || { echo "pmc $name failed"; exit 1; }
 }
 for kind in ${PMC_KINDS:-uniform contention}; do

@@ -27,12 +27,20 @@ kind, kname, out = sys.argv[1], sys.argv[2], sys.argv[3]
 agg = collections.defaultdict(float)
 dur = {}
 for d in sys.argv[4:]:
+    # one dispatch per pass: the first launch of the kernel at its largest grid (the workload's
+    # first-tier launch; a pass's process may also launch the same kernel for other rows)
+    rows = []
     for f in sorted(glob.glob(f"{d}/**/*.csv", recursive=True)):
-        for row in csv.DictReader(open(f)):
-            if "Counter_Name" not in row or kname not in row["Kernel_Name"]:
-                continue
-            agg[row["Counter_Name"]] += float(row["Counter_Value"])
-            dur[row["Counter_Name"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
+        rows += [r for r in csv.DictReader(open(f)) if "Counter_Name" in r and kname in r["Kernel_Name"]]
+    if not rows:
+        continue
+    grid = max(int(r["Grid_Size"]) for r in rows)
+    first = min(int(r["Dispatch_Id"]) for r in rows if int(r["Grid_Size"]) == grid)
+    for row in rows:
+        if int(row["Dispatch_Id"]) != first:
+            continue
+        agg[row["Counter_Name"]] += float(row["Counter_Value"])
+        dur[row["Counter_Name"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
 res = {"kernel": kname, "workload": kind, "source": " ".join(sys.argv[4:]),
        "kernel_fingerprint": kernel_fingerprint.fingerprint(os.environ.get("DASH_LIB") or kernel_fingerprint.LIB)}
 for k in sorted(agg):

@@ -312,7 +312,7 @@ def box_record(before, after):
         after.pop("_dev", None)
     out = {"probe_before": before, "probe_after": after,
            "probe_basis": "dash_probe_box: CUs x 8 workgroups x 256 threads, 8 dependent full-rate VALU chains "
-                          "per lane, 2^18 trips; sclk = shader-clock cycles (s_memtime) / 100-MHz reference ticks "
+                          "per lane, 2^21 trips (~170 ms); sclk = shader-clock cycles (s_memtime) / 100-MHz reference ticks "
                           "(s_memrealtime) over each workgroup's loop"}
     if dev:
         out["device"] = {k: dev[k] for k in ("name", "arch", "compute_units", "clock_khz", "mem_clock_khz",

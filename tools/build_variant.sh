@@ -7,7 +7,7 @@ set -euo pipefail
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/ue22cs343bb1-openmp-assignment_amd
-OUT=$ROOT/tools/variants; mkdir -p "$OUT"
+OUT=${OUT:-$ROOT/tools/variants}; mkdir -p "$OUT"
 HIPCC=/opt/rocm/bin/hipcc
 SRC=${SRC:-$PKG/csrc/dash_kernels.hip}
 if [ -n "${PATCHES:-}" ]; then

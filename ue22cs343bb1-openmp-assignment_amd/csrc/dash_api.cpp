@@ -796,7 +796,9 @@ int dash_probe_box(int device, dash_box_probe* out) {
         out->pci_device = p.pciDeviceID;
         out->total_mem = p.totalGlobalMem;
         const uint32_t blocks = (uint32_t)std::max(1, p.multiProcessorCount) * 8u;
-        const uint32_t iters = 1u << 18;  // ~15 ms at 2.4 GHz (2 wave64 VALU per cycle per CU)
+        // ~170 ms at 2.4 GHz (2 wave64 VALU per cycle per CU): long enough for the clock to settle
+    // (a 20-ms probe measured 1.88 GHz on a box whose sysfs clock read 2.39 GHz under load)
+    const uint32_t iters = 1u << 21;
         uint32_t* sink = nullptr;
         unsigned long long* clk = nullptr;
         hipStream_t st = nullptr;

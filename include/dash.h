@@ -89,7 +89,7 @@ typedef struct dash_cfg {
                              0 = 1024 + 256*max_instr */
     int32_t device;       /* HIP device ordinal */
     uint32_t trace_events; /* per-node event log capacity for DEBUG_MSG / DEBUG_INSTR
-                              emission (ref :179-182, :649-652); 0 = no log */
+                              emission (ref :179-182, :649-652); 0 = no log; < 2^30 */
     uint64_t schedule_seed; /* 0: lowest-sender-first lockstep (the parity schedule); else a
                                seeded legal schedule: per round a node sits out w.p. 1/4 and
                                senders deliver in a seeded order */

@@ -172,6 +172,8 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
         return invalid("dash_create: num_systems above 2^32 - 1");
     if (cfg->trace_events && (double)cfg->num_systems * N * cfg->trace_events * 8.0 > 64.0 * (1ull << 30))
         return invalid("dash_create: event log larger than 64 GiB");
+    if (cfg->trace_events >= (1u << 30))  // the event-log kernel packs a log position in 30 bits
+        return invalid("dash_create: trace_events must be below 2^30");
     dash_t* h = new (std::nothrow) dash_ctx();
     if (!h) {
         set_global_msg("dash_create: out of host memory");

@@ -120,10 +120,12 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
     static constexpr uint32_t WORDS = WND + WIN * WCHUNK * 64 / 2;
-    // the event-log kernel (MODE 2) only: this trip's events, u32 [64 lanes][4 slots][2], 16-B
-    // aligned (WORDS is odd for some instantiations; the staging accesses are 8-B ds ops)
-    static constexpr uint32_t EVS = (WORDS + 3u) & ~3u;
-    static constexpr uint32_t EVS_WORDS = 64 * 4 * 2;
+    // the event-log kernels (MODE 2, 3) only: the events of the last two rounds, one u32 per lane
+    // and slot (payload | round parity << 24 | issued << 31): 512 B, so the kernel keeps 17 waves
+    // per CU (a 2-KB, 4-round staging area cost three waves and 40 % of its time)
+    static constexpr uint32_t EVS = WORDS;
+    static constexpr uint32_t EVS_SLOTS = 2;
+    static constexpr uint32_t EVS_WORDS = 64 * EVS_SLOTS;
 };
 
 __device__ __forceinline__ void chunk_words(uint2 v, uint32_t& x, uint32_t& y) { x = v.x; y = v.y; }
@@ -168,9 +170,10 @@ __device__ __forceinline__ mask_t Mbit15(uint32_t v) {
 //   1 = a seeded legal schedule (a.arb_seed != 0, DESIGN.md §2 -- per round, a node sits out
 //       with probability 1/4 and senders deliver in a seeded affine order; oracle twins
 //       orc_arb_stall, orc_arb_prio);
-//   2 = the DEBUG_MSG / DEBUG_INSTR event log (a.events), lockstep or seeded (tested at run
-//       time).
-// Mode 1 without the event-log code keeps its loop free of SGPR spill reloads.
+//   2 = the DEBUG_MSG / DEBUG_INSTR event log (a.events) under lockstep;
+//   3 = the event log under a seeded (or explicit) schedule.
+// Mode 1 without the event-log code keeps its loop free of SGPR spill reloads; the schedule is a
+// compile-time property of every mode (a run-time test in the event-log kernel cost it 12 %).
 template <int P, int CS, uint32_t RING, int MODE>
 __global__ __launch_bounds__(64)
 #if DASH_WAVES_PER_EU
@@ -178,13 +181,13 @@ __attribute__((amdgpu_waves_per_eu(DASH_WAVES_PER_EU)))
 #endif
 void sim_kernel(const SimArgs a) {
     constexpr bool SLOW = MODE != 0;
-    // the seeded schedule is on (compile-time in modes 0 and 1)
-    const bool ARB = MODE == 1 || (MODE == 2 && a.arb_seed != 0);
+    constexpr bool ARB = MODE == 1 || MODE == 3;  // the seeded / explicit schedule is on
+    constexpr bool EVLOG = MODE >= 2;              // the DEBUG event log is on
     using L = Lds<P, CS, RING>;
     const uint32_t ncs = CS ? (uint32_t)CS : a.cache_size;  // cache lines per node
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[MODE == 2 ? L::EVS + L::EVS_WORDS : L::WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[EVLOG ? L::EVS + L::EVS_WORDS : L::WORDS];
     uint16_t* const lds16 = reinterpret_cast<uint16_t*>(lds);
 
     const uint32_t lane = threadIdx.x;
@@ -410,11 +413,15 @@ void sim_kernel(const SimArgs a) {
         // the popped message's type, or 13 (no transactionType) for a lane that does not pop:
         // the type masks below then need no AND with mHas
         const uint32_t pty = B(mHas) ? mty : 13u;
-        if (MODE == 2) {  // the event log (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652): staged in LDS
+        // the event log (ref DEBUG_MSG :179-182, DEBUG_INSTR :649-652), staged in LDS; a plain `if`
+        // with the COLD() barrier, not `if constexpr`: the fast kernel's code stays byte-identical
+        if (EVLOG) {
             COLD();
             if (B(mHas | mDo)) {
-                uint2* const es = reinterpret_cast<uint2*>(ldsb + L::EVS * 4) + lane * 4 + nb;
-                *es = make_uint2((rv + k) | (B(mHas) ? 0u : 0x80000000u), B(mHas) ? m : ins);  // bit 31: issued
+                // message words use bits 0..23 and 28..30 (dash_read_events drops 7 and 15);
+                // instruction words 0..15: bit 24 keeps the round's parity, bit 31 the kind
+                lds[L::EVS + lane * L::EVS_SLOTS + nb] =
+                    (B(mHas) ? (m & 0x70FFFFFFu) : (ins | 0x80000000u)) | ((k & 1u) << 24);
                 ++nb;
                 ++nev;
             }
@@ -651,27 +658,6 @@ void sim_kernel(const SimArgs a) {
         }
     };
 
-    // MODE 2: write the trip's staged events (at most one per round, so <= 4 per node) to the
-    // nodes' logs. Each node's events of a trip are contiguous in its log (positions nev - nb ..
-    // nev - 1); four lanes write one node's four 8-B slots, so one store instruction covers 16
-    // nodes' 32-B runs (16 lines) instead of 64 lanes' 8 B in 64 lines per round.
-    auto flush_events = [&]() __attribute__((always_inline)) {
-        asm volatile("" ::: "memory");  // the staging writes before the cross-lane reads
-        const uint32_t first = nev - nb;
-        const uint64_t lbase = (sys * N + t) * (uint64_t)a.event_cap;
-        const uint2* const es = reinterpret_cast<const uint2*>(ldsb + L::EVS * 4);
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t n = q * 16 + (lane >> 2), slot = lane & 3u;
-            const uint32_t nbn = __shfl(nb, (int)n), fn = __shfl(first, (int)n);
-            const uint64_t lb = __shfl(lbase, (int)n);
-            if (slot < nbn && fn + slot < a.event_cap)
-                *reinterpret_cast<uint2*>(a.events + (lb + fn + slot) * 2) = es[n * 4 + slot];
-        }
-        asm volatile("" ::: "memory");
-        nb = 0;
-    };
-
     // TRIP rounds per trip of WCHUNK-round blocks, unrolled; the trip's start is the
     // housekeeping point (quiescence vote, overflow stop), each block's start the round-cap
     // test and the trace window refill
@@ -714,7 +700,50 @@ void sim_kernel(const SimArgs a) {
         }
         step(0, mMsg, mIss);
 #pragma unroll
-        for (uint32_t k = 1; k < WCHUNK; ++k) step(k, can_pop(), can_issue());
+        for (uint32_t k = 1; k < WCHUNK; ++k) {
+            step(k, can_pop(), can_issue());
+            // MODE 2, 3: after rounds k - 1 and k, write their staged events (at most one per
+            // round, so <= 2 per node) to the nodes' logs. A node's events are contiguous in its
+            // log (positions nev - nb .. nev - 1); two lanes write one node's two 8-B slots, so one
+            // store instruction covers 32 nodes' 16-B runs instead of 64 lanes' 8 B in 64 lines
+            // per round. A node's log base comes from its lane (a shuffle only on the rare re-runs
+            // of a deeper queue tier, whose systems come from a list); its count and first
+            // position travel in one shuffle. (Inline, not a lambda: the fast kernel's code stays
+            // byte-identical.)
+            if constexpr (EVLOG) {
+                if (k % 2u == 1u) {
+                    asm volatile("" ::: "memory");  // the staging writes before the cross-lane reads
+                    const uint32_t cap = a.event_cap;
+                    const uint32_t first = nev - nb;
+                    // count and first position of the pending events; 0 when none can be stored
+                    // (cap < 2^30, dash_create)
+                    const uint32_t pk = (nb != 0u && first < cap) ? ((first << 2) | nb) : 0u;
+                    const uint64_t lbase = (sys * N + t) * (uint64_t)cap;
+#pragma unroll
+                    for (uint32_t q = 0; q < L::EVS_SLOTS; ++q) {  // 64 / EVS_SLOTS nodes per pass
+                        const uint32_t n = q * (64u / L::EVS_SLOTS) + lane / L::EVS_SLOTS;
+                        const uint32_t slot = lane % L::EVS_SLOTS;
+                        const uint32_t pn = __shfl(pk, (int)n);
+                        uint64_t lb;
+                        if (a.sys_list) {
+                            COLD();
+                            lb = __shfl(lbase, (int)n);
+                        } else {
+                            lb = ((slot_id - lane / P + n / P) * N + (n & (P - 1u))) * (uint64_t)cap;
+                        }
+                        const uint32_t fn = pn >> 2, nbn = pn & 3u;
+                        if (slot < nbn && fn + slot < cap) {
+                            const uint32_t w = lds[L::EVS + n * L::EVS_SLOTS + slot];
+                            const uint32_t round = rv + (k - 1u) + ((w >> 24) & 1u);
+                            *reinterpret_cast<uint2*>(a.events + (lb + fn + slot) * 2) =
+                                make_uint2(round | (w & 0x80000000u), w & 0x70FFFFFFu);
+                        }
+                    }
+                    asm volatile("" ::: "memory");
+                    nb = 0;
+                }
+            }
+        }
         if constexpr (TRIP == 2 * WCHUNK) {
             mMsg = can_pop();
             mIss = can_issue();
@@ -724,7 +753,6 @@ void sim_kernel(const SimArgs a) {
 #pragma unroll
             for (uint32_t k = WCHUNK + 1; k < TRIP; ++k) step(k, can_pop(), can_issue());
         }
-        if constexpr (MODE == 2) flush_events();
         rv += TRIP;
         mMsg = can_pop();
         mIss = can_issue();
@@ -874,7 +902,9 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
 
 template <int P, int CS, uint32_t RING>
 static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t s) {
-    if (a.events)
+    if (a.events && a.arb_seed)
+        hipLaunchKernelGGL((sim_kernel<P, CS, RING, 3>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+    else if (a.events)
         hipLaunchKernelGGL((sim_kernel<P, CS, RING, 2>), dim3((uint32_t)groups), dim3(64), 0, s, a);
     else if (a.arb_seed)
         hipLaunchKernelGGL((sim_kernel<P, CS, RING, 1>), dim3((uint32_t)groups), dim3(64), 0, s, a);

@@ -125,7 +125,8 @@ struct Lds {  // 32-bit word offsets
     // per CU (a 2-KB, 4-round staging area cost three waves and 40 % of its time)
     static constexpr uint32_t EVS = WORDS;
     static constexpr uint32_t EVS_SLOTS = 2;
-    static constexpr uint32_t EVS_WORDS = 64 * EVS_SLOTS;
+    static constexpr uint32_t EVP = EVS + 64 * EVS_SLOTS;  // u32 [64]: each node's count | first << 2
+    static constexpr uint32_t EVS_WORDS = 64 * EVS_SLOTS + 64;
 };
 
 __device__ __forceinline__ void chunk_words(uint2 v, uint32_t& x, uint32_t& y) { x = v.x; y = v.y; }
@@ -210,6 +211,18 @@ void sim_kernel(const SimArgs a) {
         sys = slot_id;
     }
     uint32_t len = live ? a.lens[sys * N + t] : 0u;
+    // event-log kernels: the log of the node each lane writes in flush pass q (node q * 32 +
+    // lane / 2, see the flush after every second round), fixed for the whole run
+    uint32_t* evlog[L::EVS_SLOTS] = {};
+    if (EVLOG) {
+        COLD();
+#pragma unroll
+        for (uint32_t q = 0; q < L::EVS_SLOTS; ++q) {
+            const uint32_t n = q * (64u / L::EVS_SLOTS) + lane / L::EVS_SLOTS;
+            const uint64_t sys_n = __shfl(sys, (int)n);
+            evlog[q] = a.events + (sys_n * N + (n & (P - 1u))) * (uint64_t)a.event_cap * 2u;
+        }
+    }
     const uint32_t rcv_mask = (1u << N) - 1u;
 
     // initializeProcessor's state part (ref :808-820); directory/line states
@@ -706,36 +719,27 @@ void sim_kernel(const SimArgs a) {
             // round, so <= 2 per node) to the nodes' logs. A node's events are contiguous in its
             // log (positions nev - nb .. nev - 1); two lanes write one node's two 8-B slots, so one
             // store instruction covers 32 nodes' 16-B runs instead of 64 lanes' 8 B in 64 lines
-            // per round. A node's log base comes from its lane (a shuffle only on the rare re-runs
-            // of a deeper queue tier, whose systems come from a list); its count and first
-            // position travel in one shuffle. (Inline, not a lambda: the fast kernel's code stays
+            // per round. The nodes' log bases are computed once (evlog); each node's count and first
+            // position go through LDS. (Inline, not a lambda: the fast kernel's code stays
             // byte-identical.)
             if constexpr (EVLOG) {
                 if (k % 2u == 1u) {
-                    asm volatile("" ::: "memory");  // the staging writes before the cross-lane reads
                     const uint32_t cap = a.event_cap;
                     const uint32_t first = nev - nb;
                     // count and first position of the pending events; 0 when none can be stored
                     // (cap < 2^30, dash_create)
-                    const uint32_t pk = (nb != 0u && first < cap) ? ((first << 2) | nb) : 0u;
-                    const uint64_t lbase = (sys * N + t) * (uint64_t)cap;
+                    lds[L::EVP + lane] = (nb != 0u && first < cap) ? ((first << 2) | nb) : 0u;
+                    asm volatile("" ::: "memory");  // the staging writes before the cross-lane reads
 #pragma unroll
                     for (uint32_t q = 0; q < L::EVS_SLOTS; ++q) {  // 64 / EVS_SLOTS nodes per pass
                         const uint32_t n = q * (64u / L::EVS_SLOTS) + lane / L::EVS_SLOTS;
                         const uint32_t slot = lane % L::EVS_SLOTS;
-                        const uint32_t pn = __shfl(pk, (int)n);
-                        uint64_t lb;
-                        if (a.sys_list) {
-                            COLD();
-                            lb = __shfl(lbase, (int)n);
-                        } else {
-                            lb = ((slot_id - lane / P + n / P) * N + (n & (P - 1u))) * (uint64_t)cap;
-                        }
+                        const uint32_t pn = lds[L::EVP + n];
                         const uint32_t fn = pn >> 2, nbn = pn & 3u;
                         if (slot < nbn && fn + slot < cap) {
                             const uint32_t w = lds[L::EVS + n * L::EVS_SLOTS + slot];
                             const uint32_t round = rv + (k - 1u) + ((w >> 24) & 1u);
-                            *reinterpret_cast<uint2*>(a.events + (lb + fn + slot) * 2) =
+                            *reinterpret_cast<uint2*>(evlog[q] + (fn + slot) * 2u) =
                                 make_uint2(round | (w & 0x80000000u), w & 0x70FFFFFFu);
                         }
                     }

@@ -1411,16 +1411,21 @@ typedef struct {
 
 static int g_cursor(const xsys *s, int t) { return (int)s->n[t].idx + (int)s->npop[t]; }
 
+/* A node pops while its queue is non-empty and its queue is FIFO, so every queued message must
+ * be the node's next logged pops, in order, with no logged issue among them (the whole queue,
+ * not only its head: a wrong message behind the head can never leave without a mismatch). */
 static int g_dead(const xctx *c, const xguide *g, const xsys *s) {
     for (int t = 0; t < c->N; t++) {
         const xnode *x = &s->n[t];
-        if (x->qn == 0) continue;
         const int k = g_cursor(s, t);
-        if ((uint32_t)k >= g->n[t]) return 1;
-        const uint32_t e = g->ev[t][k];
-        if (e >> 31) return 1;
-        const omsg *h = &x->q[0];
-        if ((e & 0xFF) != h->type || ((e >> 8) & 0xFF) != h->sender || ((e >> 16) & 0xFF) != h->address) return 1;
+        if ((uint64_t)k + x->qn > g->n[t]) return 1;
+        for (int i = 0; i < (int)x->qn; i++) {
+            const uint32_t e = g->ev[t][k + i];
+            const omsg *h = &x->q[i];
+            if ((e >> 31) || (e & 0xFF) != h->type || ((e >> 8) & 0xFF) != h->sender ||
+                ((e >> 16) & 0xFF) != h->address)
+                return 1;
+        }
     }
     return 0;
 }

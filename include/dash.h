@@ -88,8 +88,11 @@ typedef struct dash_cfg {
                              clamped to 2^31 - 4, then rounded up to a multiple of 4;
                              0 = 1024 + 256*max_instr */
     int32_t device;       /* HIP device ordinal */
-    uint32_t trace_events; /* per-node event log capacity for DEBUG_MSG / DEBUG_INSTR
-                              emission (ref :179-182, :649-652); 0 = no log; < 2^30 */
+    uint32_t trace_events; /* event log capacity for DEBUG_MSG / DEBUG_INSTR emission
+                              (ref :179-182, :649-652), in rounds: every node's events of the
+                              first trace_events rounds (a node logs at most one event per
+                              round, so also at most trace_events events per node); 0 = no
+                              log; < 2^30; device memory num_systems x num_procs x 4 B each */
     uint64_t schedule_seed; /* 0: lowest-sender-first lockstep (the parity schedule); else a
                                seeded legal schedule: per round a node sits out w.p. 1/4 and
                                senders deliver in a seeded order */
@@ -195,7 +198,8 @@ int dash_read_results(dash_t *h, uint64_t first, uint64_t count, uint64_t *diges
                       uint32_t *rounds, uint32_t *errors);
 int dash_read_hist(dash_t *h, uint64_t sys, uint32_t *hist /* [DASH_NUM_TXN] */);
 /* The event log of one system, merged in lockstep order (round, then node): up to
-   cap events into out, the total into *n. DASH_ETRUNC if a node's log overflowed. */
+   cap events into out, the total into *n. DASH_ETRUNC if events fell past the log's
+   trace_events rounds (counted in *n, not kept). */
 int dash_read_events(dash_t *h, uint64_t sys, dash_event *out, uint32_t cap, uint32_t *n);
 /* HIP stream the engine launches on (hipStream_t as void*) */
 void *dash_stream(dash_t *h);

@@ -38,10 +38,11 @@ struct dash_ctx {
     unsigned long long* d_stats = nullptr;
     uint32_t* d_list[2] = {nullptr, nullptr};  // overflow hand-off lists (ping-pong)
     uint32_t* d_count = nullptr;
-    uint32_t* d_events = nullptr;       // [(sys*N+node)*trace_events][2]
+    uint32_t* d_events = nullptr;       // [sys][round / 4][node][round % 4] (rounds: ev_rounds)
     uint32_t* d_arb = nullptr;          // seeded schedule: one word per node and round (dash::arb_node)
     uint32_t arb_len = 0;
     uint32_t* d_event_count = nullptr;  // [sys*N+node]
+    uint32_t ev_rounds = 0;             // trace_events rounded up to a multiple of 4
     uint64_t tier_systems[dash::NUM_TIERS] = {};  // systems run per queue-depth tier, last run
     int auto_tier = 0;                         // adaptive first tier
     // overflow hint: the systems that overflowed the first tier in earlier
@@ -170,10 +171,10 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     if (cfg->max_instr > (1u << 24)) return invalid("dash_create: max_instr above 2^24");
     if (cfg->num_systems > 0xFFFFFFFFull)  // system ids are u32 in the lists
         return invalid("dash_create: num_systems above 2^32 - 1");
-    if (cfg->trace_events && (double)cfg->num_systems * N * cfg->trace_events * 8.0 > 64.0 * (1ull << 30))
-        return invalid("dash_create: event log larger than 64 GiB");
-    if (cfg->trace_events >= (1u << 30))  // the event-log kernel packs a log position in 30 bits
+    if (cfg->trace_events >= (1u << 30))
         return invalid("dash_create: trace_events must be below 2^30");
+    if (cfg->trace_events && (double)cfg->num_systems * N * (cfg->trace_events + 3u) * 4.0 > 64.0 * (1ull << 30))
+        return invalid("dash_create: event log larger than 64 GiB");
     dash_t* h = new (std::nothrow) dash_ctx();
     if (!h) {
         set_global_msg("dash_create: out of host memory");
@@ -235,7 +236,8 @@ int dash_create(const dash_cfg* cfg, dash_t** out) {
     chk(hipMalloc(&h->d_skip, std::max<uint64_t>(nsys, 1)), "hipMalloc(skip)");
     if (rc == DASH_OK) chk(hipMemset(h->d_skip, 0, std::max<uint64_t>(nsys, 1)), "hipMemset(skip)");
     if (cfg->trace_events) {
-        chk(hipMalloc(&h->d_events, std::max<uint64_t>(nsys * N * cfg->trace_events, 1) * 8), "hipMalloc(events)");
+        h->ev_rounds = (cfg->trace_events + 3u) & ~3u;
+        chk(hipMalloc(&h->d_events, std::max<uint64_t>(nsys * N * h->ev_rounds, 1) * 4), "hipMalloc(events)");
         chk(hipMalloc(&h->d_event_count, std::max<uint64_t>(nsys * N, 1) * 4), "hipMalloc(event_count)");
     }
     if (cfg->schedule_seed) {  // the seeded schedule's round words, built once per handle
@@ -399,7 +401,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
     a.state = h->d_state;
     a.hist = h->d_hist;
     a.keep = (h->cfg.flags & DASH_KEEP_STATE) ? 1u : 0u;
-    a.event_cap = h->cfg.trace_events;
+    a.event_cap = h->ev_rounds;
     a.arb_seed = h->cfg.schedule_seed;
     a.arb_tab = h->d_arb;
     a.arb_len = h->arb_len;
@@ -575,47 +577,37 @@ int dash_read_events(dash_t* h, uint64_t sys, dash_event* out, uint32_t cap, uin
         if (!h->ran) return fail(h, DASH_ESTATE, "dash_run has not completed");
         if (!h->d_events) return fail(h, DASH_ESTATE, "created with trace_events = 0");
         if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
-        const uint32_t N = h->cfg.num_procs, E = h->cfg.trace_events;
-        std::vector<uint32_t> cnt(N), ev((size_t)N * E * 2);
+        const uint32_t N = h->cfg.num_procs, R = h->ev_rounds;
+        std::vector<uint32_t> cnt(N), ev((size_t)N * R);
         HIPCHK(h, hipSetDevice(h->cfg.device));
         HIPCHK(h, hipMemcpyAsync(cnt.data(), h->d_event_count + sys * N, N * 4, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipMemcpyAsync(ev.data(), h->d_events + sys * N * E * 2, ev.size() * 4, hipMemcpyDeviceToHost,
+        HIPCHK(h, hipMemcpyAsync(ev.data(), h->d_events + sys * N * (uint64_t)R, ev.size() * 4, hipMemcpyDeviceToHost,
                                  h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
-        // merge the per-node logs (each in round order) by (round, node): a node logs at
-        // most one event per round, so this is the lockstep order
-        std::vector<uint32_t> pos(N, 0);
-        bool trunc = false;
-        uint64_t total = 0;
-        for (uint32_t t = 0; t < N; t++) {
-            total += cnt[t];
-            if (cnt[t] > E) trunc = true;
-        }
+        // the log is round-major (a node logs at most one event per round): reading it round by
+        // round, node by node, is the lockstep order
+        uint64_t total = 0, logged = 0;
+        for (uint32_t t = 0; t < N; t++) total += cnt[t];
         uint32_t k = 0;
-        for (;;) {
-            int best = -1;
+        for (uint32_t r = 0; r < R; r++)
             for (uint32_t t = 0; t < N; t++) {
-                if (pos[t] >= std::min(cnt[t], E)) continue;
-                if (best < 0 || (ev[((size_t)t * E + pos[t]) * 2] & 0x7FFFFFFFu) <
-                                    (ev[((size_t)best * E + pos[best]) * 2] & 0x7FFFFFFFu))
-                    best = (int)t;
+                const uint32_t w = ev[(size_t)(r / 4) * N * 4 + t * 4 + r % 4];
+                if (!(w & 0x01000000u)) continue;  // bit 24: an event
+                ++logged;
+                if (k < cap) {
+                    out[k].round = r;
+                    out[k].node = t;
+                    out[k].kind = (w & 0x80000000u) ? DASH_EV_INSTR : DASH_EV_MSG;
+                    // a message word without the kernel's internal bits (7: REPLY_RD's dirState,
+                    // 15: the reply-table flag, 24) and with secondReceiver moved from bits 30..28
+                    // to 26..24, as include/dash.h documents it
+                    out[k].word = (w & 0x80000000u) ? (w & 0xFFFFu) : (w & 0x00FF7F7Fu) | (((w >> 28) & 7u) << 24);
+                }
+                ++k;
             }
-            if (best < 0) break;
-            const uint32_t* e = &ev[((size_t)best * E + pos[best]) * 2];
-            if (k < cap) {
-                out[k].round = e[0] & 0x7FFFFFFFu;  // bit 31: an issued instruction
-                out[k].node = (uint32_t)best;
-                out[k].kind = (e[0] & 0x80000000u) ? DASH_EV_INSTR : DASH_EV_MSG;
-                // a message word without the kernel's internal bits (7: REPLY_RD's dirState,
-                // 15: the reply-table flag, 27..24) and with secondReceiver moved from bits 30..28
-                // to 26..24, as include/dash.h documents it
-                out[k].word = (e[0] & 0x80000000u) ? e[1] : (e[1] & 0x00FF7F7Fu) | (((e[1] >> 28) & 7u) << 24);
-            }
-            ++k;
-            ++pos[best];
-        }
+        const bool trunc = logged < total;  // events past the log's rounds were counted, not stored
         *n = (uint32_t)std::min<uint64_t>(total, 0xFFFFFFFFull);
-        return trunc ? fail(h, DASH_ETRUNC, "event log truncated at %u events per node", E) : DASH_OK;
+        return trunc ? fail(h, DASH_ETRUNC, "event log truncated at %u rounds", R) : DASH_OK;
     });
 }
 

@@ -46,8 +46,8 @@ struct SimArgs {
     uint32_t* state;          // optional [(sys*N+node)*(16+CS)] directory/cache words
     uint32_t* hist;           // [sys*13] messages handled per type; written when keep
     uint32_t keep;
-    uint32_t event_cap;       // per-node event log capacity (0: no log)
-    uint32_t* events;         // [(sys*N+node)*event_cap][2]: round, word (bit 31: issued instruction)
+    uint32_t event_cap;       // event log capacity in rounds, a multiple of 4 (0: no log)
+    uint32_t* events;         // [sys][round / 4][node][round % 4]: one word per node and round, 0 = none
     uint32_t* event_count;    // [sys*N+node] events produced (may exceed event_cap)
     unsigned long long* stats;  // [STAT_WORDS]
     uint64_t arb_seed;        // 0: lowest-sender-first lockstep; else the seeded schedule

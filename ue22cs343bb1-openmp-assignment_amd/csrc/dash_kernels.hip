@@ -120,13 +120,6 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
     static constexpr uint32_t WORDS = WND + WIN * WCHUNK * 64 / 2;
-    // the event-log kernels (MODE 2, 3) only: the events of the last two rounds, one u32 per lane
-    // and slot (payload | round parity << 24 | issued << 31): 512 B, so the kernel keeps 17 waves
-    // per CU (a 2-KB, 4-round staging area cost three waves and 40 % of its time)
-    static constexpr uint32_t EVS = WORDS;
-    static constexpr uint32_t EVS_SLOTS = 2;
-    static constexpr uint32_t EVP = EVS + 64 * EVS_SLOTS;  // u32 [64]: each node's count | first << 2
-    static constexpr uint32_t EVS_WORDS = 64 * EVS_SLOTS + 64;
 };
 
 __device__ __forceinline__ void chunk_words(uint2 v, uint32_t& x, uint32_t& y) { x = v.x; y = v.y; }
@@ -188,7 +181,7 @@ void sim_kernel(const SimArgs a) {
     const uint32_t ncs = CS ? (uint32_t)CS : a.cache_size;  // cache lines per node
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[EVLOG ? L::EVS + L::EVS_WORDS : L::WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS];
     uint16_t* const lds16 = reinterpret_cast<uint16_t*>(lds);
 
     const uint32_t lane = threadIdx.x;
@@ -211,17 +204,12 @@ void sim_kernel(const SimArgs a) {
         sys = slot_id;
     }
     uint32_t len = live ? a.lens[sys * N + t] : 0u;
-    // event-log kernels: the log of the node each lane writes in flush pass q (node q * 32 +
-    // lane / 2, see the flush after every second round), fixed for the whole run
-    uint32_t* evlog[L::EVS_SLOTS] = {};
+    // event-log kernels: this node's column of its system's round-major log (four rounds of the
+    // system's N nodes per 16N-B row, this node's 16 B at column t), written one row per four rounds
+    uint4* evq = nullptr;
     if (EVLOG) {
         COLD();
-#pragma unroll
-        for (uint32_t q = 0; q < L::EVS_SLOTS; ++q) {
-            const uint32_t n = q * (64u / L::EVS_SLOTS) + lane / L::EVS_SLOTS;
-            const uint64_t sys_n = __shfl(sys, (int)n);
-            evlog[q] = a.events + (sys_n * N + (n & (P - 1u))) * (uint64_t)a.event_cap * 2u;
-        }
+        evq = reinterpret_cast<uint4*>(a.events + sys * N * (uint64_t)a.event_cap) + t;
     }
     const uint32_t rcv_mask = (1u << N) - 1u;
 
@@ -287,7 +275,7 @@ void sim_kernel(const SimArgs a) {
     uint32_t err = 0, maxd = 0, drops = 0;  // maxd in ring-slot bytes until the end
     uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
     uint32_t nev = 0;         // events logged (DEBUG_MSG / DEBUG_INSTR emission, off unless a.events)
-    uint32_t nb = 0;          // of which staged in LDS this trip, not yet written (MODE 2)
+    uint32_t ev0 = 0, ev1 = 0, ev2 = 0, ev3 = 0;  // this node's log words of the current four rounds (MODE 2, 3)
     // loop-invariant uniform values a round needs, kept in VGPRs: the round's lane masks
     // need the SGPRs (spilling them costs VALU)
     // rcv_all: the nodes a REPLY_ID fan-out reaches (every node of the system but this one:
@@ -430,14 +418,13 @@ void sim_kernel(const SimArgs a) {
         // with the COLD() barrier, not `if constexpr`: the fast kernel's code stays byte-identical
         if (EVLOG) {
             COLD();
-            if (B(mHas | mDo)) {
-                // message words use bits 0..23 and 28..30 (dash_read_events drops 7 and 15);
-                // instruction words 0..15: bit 24 keeps the round's parity, bit 31 the kind
-                lds[L::EVS + lane * L::EVS_SLOTS + nb] =
-                    (B(mHas) ? (m & 0x70FFFFFFu) : (ins | 0x80000000u)) | ((k & 1u) << 24);
-                ++nb;
-                ++nev;
-            }
+            // one word per node and round: 0 = no event; else bit 24 set, bit 31 the kind, the
+            // message word in bits 0..23 and 28..30 (dash_read_events drops 7 and 15) or the
+            // instruction in bits 0..15
+            const uint32_t evx = B(mHas) ? ((m & 0x70FFFFFFu) | 0x01000000u) : B(mDo) ? (ins | 0x81000000u) : 0u;
+            // (named words, not an array indexed by k % 4: the fast kernel's code stays the same)
+            (k % 4u == 0u ? ev0 : k % 4u == 1u ? ev1 : k % 4u == 2u ? ev2 : ev3) = evx;
+            nev += B(mHas | mDo) ? 1u : 0u;
         }
         // messages handled per transactionType, per system; a lane without a message counts
         // into row 13 (pty = 13), so no exec mask is needed (more LDS bank conflicts on that
@@ -671,12 +658,20 @@ void sim_kernel(const SimArgs a) {
         }
     };
 
+    // MODE 2, 3: after round k (k % 4 == 3), this node's words of rounds k - 3 .. k, one 16-B store
+    // (a system's N nodes fill 16N contiguous bytes: whole lines at N = 8); rounds past the log's
+    // capacity are counted (nev), not stored
+    auto store_events = [&](const uint32_t r0) __attribute__((always_inline)) {
+        if (live && r0 < a.event_cap) evq[(r0 / 4u) * N] = make_uint4(ev0, ev1, ev2, ev3);
+    };
+
     // TRIP rounds per trip of WCHUNK-round blocks, unrolled; the trip's start is the
     // housekeeping point (quiescence vote, overflow stop), each block's start the round-cap
     // test and the trace window refill
     constexpr uint32_t TRIP = DASH_QCHECK;
     static_assert(TRIP == WCHUNK || TRIP == 2 * WCHUNK, "one or two refill blocks per trip");
     static_assert(!SLOW || TRIP == 4, "the seeded schedule reads four round words per trip");
+    static_assert(!EVLOG || TRIP % 4 == 0, "event rows end at trip ends");
     mask_t mMsg = can_pop(), mIss = can_issue();
     // quiescence is absorbing, so testing it once per trip only adds idle rounds (no
     // state changes, not counted in `rounds`)
@@ -715,38 +710,8 @@ void sim_kernel(const SimArgs a) {
 #pragma unroll
         for (uint32_t k = 1; k < WCHUNK; ++k) {
             step(k, can_pop(), can_issue());
-            // MODE 2, 3: after rounds k - 1 and k, write their staged events (at most one per
-            // round, so <= 2 per node) to the nodes' logs. A node's events are contiguous in its
-            // log (positions nev - nb .. nev - 1); two lanes write one node's two 8-B slots, so one
-            // store instruction covers 32 nodes' 16-B runs instead of 64 lanes' 8 B in 64 lines
-            // per round. The nodes' log bases are computed once (evlog); each node's count and first
-            // position go through LDS. (Inline, not a lambda: the fast kernel's code stays
-            // byte-identical.)
-            if constexpr (EVLOG) {
-                if (k % 2u == 1u) {
-                    const uint32_t cap = a.event_cap;
-                    const uint32_t first = nev - nb;
-                    // count and first position of the pending events; 0 when none can be stored
-                    // (cap < 2^30, dash_create)
-                    lds[L::EVP + lane] = (nb != 0u && first < cap) ? ((first << 2) | nb) : 0u;
-                    asm volatile("" ::: "memory");  // the staging writes before the cross-lane reads
-#pragma unroll
-                    for (uint32_t q = 0; q < L::EVS_SLOTS; ++q) {  // 64 / EVS_SLOTS nodes per pass
-                        const uint32_t n = q * (64u / L::EVS_SLOTS) + lane / L::EVS_SLOTS;
-                        const uint32_t slot = lane % L::EVS_SLOTS;
-                        const uint32_t pn = lds[L::EVP + n];
-                        const uint32_t fn = pn >> 2, nbn = pn & 3u;
-                        if (slot < nbn && fn + slot < cap) {
-                            const uint32_t w = lds[L::EVS + n * L::EVS_SLOTS + slot];
-                            const uint32_t round = rv + (k - 1u) + ((w >> 24) & 1u);
-                            *reinterpret_cast<uint2*>(evlog[q] + (fn + slot) * 2u) =
-                                make_uint2(round | (w & 0x80000000u), w & 0x70FFFFFFu);
-                        }
-                    }
-                    asm volatile("" ::: "memory");
-                    nb = 0;
-                }
-            }
+            if constexpr (EVLOG)
+                if (k % 4u == 3u) store_events(rv + k - 3u);
         }
         if constexpr (TRIP == 2 * WCHUNK) {
             mMsg = can_pop();
@@ -755,7 +720,11 @@ void sim_kernel(const SimArgs a) {
             refill();
             step(WCHUNK, mMsg, mIss);
 #pragma unroll
-            for (uint32_t k = WCHUNK + 1; k < TRIP; ++k) step(k, can_pop(), can_issue());
+            for (uint32_t k = WCHUNK + 1; k < TRIP; ++k) {
+                step(k, can_pop(), can_issue());
+                if constexpr (EVLOG)
+                    if (k % 4u == 3u) store_events(rv + k - 3u);
+            }
         }
         rv += TRIP;
         mMsg = can_pop();

@@ -95,7 +95,11 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
     cfg.flags = DASH_KEEP_STATE;
     cfg.num_systems = 1;
     cfg.device = dev;
-    cfg.trace_events = (dbg_instr || dbg_msg) ? 1u << 16 : 0;
+    /* the log holds every round the run may take (the default round cap, 1024 + 256 x max_instr,
+       up to 2^22): n x 4 B per round on the device */
+    uint64_t log_rounds = 1024u + 256ull * m;
+    if (log_rounds > (1u << 22)) log_rounds = 1u << 22;
+    cfg.trace_events = (dbg_instr || dbg_msg) ? (uint32_t)log_rounds : 0;
     cfg.schedule_seed = rounds ? (sched ? sched : 1) : sched;
     dash_t *h = NULL;
     int rc = dash_create(&cfg, &h);
@@ -109,8 +113,14 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
             snprintf(path, sizeof path, "%s/core_%u_output.txt", out, t);
             rc = dash_dump_file(&nodes[t], t, cs, path);
         }
-        uint32_t cap = cfg.trace_events * n, total = 0;
-        dash_event *ev = cap ? (dash_event *)malloc(sizeof(dash_event) * cap) : NULL;
+        uint32_t cap = 0, total = 0;
+        dash_event *ev = NULL;
+        if (rc == DASH_OK && cfg.trace_events) {  /* the count first, then the events */
+            int erc = dash_read_events(h, 0, NULL, 0, &cap);
+            if (erc == DASH_OK || erc == DASH_ETRUNC)
+                ev = (dash_event *)malloc(sizeof(dash_event) * (cap ? cap : 1));
+            if (!ev) rc = erc != DASH_OK ? erc : DASH_ENOMEM;
+        }
         if (rc == DASH_OK && ev) {
             int erc = dash_read_events(h, 0, ev, cap, &total);
             for (uint32_t k = 0; k < total && k < cap; k++) {

@@ -107,3 +107,27 @@ def test_rccl_collectives_one_rank():
     d1 = _line(one.stdout)
     assert dp["n_gpus"] == 1
     assert dp["totals"] == d1["totals"] and dp["contention"]["totals"] == d1["contention"]["totals"]
+
+
+def test_two_rank_line_sweep_matches_one_process():
+    """The configs[4] grid inside the headline line (`sweep`) under two ranks, as the driver's
+    N-GPU runs produce it at full size: every point's totals (all-reduced per point) equal one
+    process running all the systems, and `value` counts both ranks' instructions."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    small = ["--len", "256", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--contention-steps", "0",
+             "--line-sweep", "on", "--line-sweep-warmup", "0"]
+    two = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                          "--systems", "512"] + small, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert two.returncode == 0, two.stderr[-3000:]
+    one = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--systems", "1024"] + small,
+                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    s2, s1 = _line(two.stdout)["sweep"], _line(one.stdout)["sweep"]
+    assert len(s2["points"]) == len(s1["points"]) == 25
+    keys = ("hist", "instructions", "rounds_total", "err_systems", "dropped", "digest_sum")
+    for p2, p1 in zip(s2["points"], s1["points"]):
+        assert (p2["cache_size"], p2["locality"]) == (p1["cache_size"], p1["locality"])
+        assert {k: p2[k] for k in keys} == {k: p1[k] for k in keys}, (p2["cache_size"], p2["locality"])
+        assert p2["instructions"] == 1024 * 8 * 256
+        assert abs(p2["value"] - 1024 * 8 * 256 / (p2["ms_per_step"] / 1e3)) < 1e-6 * p2["value"]
+    assert "not this workload" in s2["golden"]["note"]

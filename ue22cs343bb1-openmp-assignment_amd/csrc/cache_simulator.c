@@ -119,7 +119,7 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
             int erc = dash_read_events(h, 0, NULL, 0, &cap);
             if (erc == DASH_OK || erc == DASH_ETRUNC)
                 ev = (dash_event *)malloc(sizeof(dash_event) * (cap ? cap : 1));
-            if (!ev) rc = erc != DASH_OK ? erc : DASH_ENOMEM;
+            if (!ev) rc = (erc == DASH_OK || erc == DASH_ETRUNC) ? DASH_ENOMEM : erc;
         }
         if (rc == DASH_OK && ev) {
             int erc = dash_read_events(h, 0, ev, cap, &total);

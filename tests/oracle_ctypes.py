@@ -155,7 +155,7 @@ def load_test_dir(d, num_procs=4, max_instr=32):
 # ---------------------------------------------------------------- runs
 
 def run_system(trace, lens, num_procs=4, cache_size=4, ring_depth=256, max_rounds=0, log=False,
-               log_msgs=False, arb_seed=0, sched=None):
+               log_msgs=False, arb_seed=0, sched=None, log_bytes=1 << 20):
     """log=True also returns the DEBUG_INSTR lines (plus DEBUG_MSG lines with
     log_msgs=True) in lockstep order (round, then node). sched: an explicit round schedule
     (uint8 [rounds][num_procs], 0xFF = sits out, else delivery position), the twin of
@@ -168,11 +168,13 @@ def run_system(trace, lens, num_procs=4, cache_size=4, ring_depth=256, max_round
         assert sched.ndim == 2 and sched.shape[1] == num_procs
         cfg.sched, cfg.sched_rounds = sched.ctypes.data, sched.shape[0]
     res = OrcResult()
-    buf = ctypes.create_string_buffer(1 << 20) if log else None
+    buf = ctypes.create_string_buffer(log_bytes) if log else None
     rc = lib().orc_run_system(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1],
-                              lens.ctypes.data, ctypes.byref(res), buf, (1 << 20) if log else 0)
+                              lens.ctypes.data, ctypes.byref(res), buf, log_bytes if log else 0)
     if rc != 0:
         raise ValueError("oracle rejected the configuration or trace")
+    if log and len(buf.value) + 64 >= log_bytes:  # the oracle stops logging 64 B before the end
+        raise ValueError(f"oracle log longer than log_bytes={log_bytes}: pass a larger buffer")
     return (res, buf.value.decode()) if log else res
 
 

@@ -278,6 +278,27 @@ def test_debug_trace_under_seeded_schedule(dash, seed):
         assert np.array_equal(eng.read_results()[0], dig_log)
 
 
+@pytest.mark.parametrize("runs", [1, 2])
+def test_debug_trace_through_queue_depth_tiers(dash, runs):
+    """The round-major event log of systems that overflow the first queue depth and are re-run
+    from scratch at the next one (16 -> 32 -> 256; on the second run of a handle the adaptive
+    first tier starts deeper): each system's log is the final run's, equal to the oracle's
+    (queue capacity 256), with nothing left over from the shallower run."""
+    ids = DEEP_SYSTEMS[:5] + [0, 1, 2]
+    L = 4096
+    packed = np.stack([oracle_ctypes.gen_system(0x5EED, s, 8, L, kind=1) for s in ids])
+    lens = np.full((len(ids), 8), L, np.uint32)
+    with dash.Engine(len(ids), num_procs=8, cache_size=4, max_instr=L, trace_events=1 << 16) as eng:
+        eng.load_traces(packed, lens)
+        for _ in range(runs):
+            st = eng.run()
+        assert st["tier_systems"][1] > 0  # some systems were re-run deeper
+        for i in range(len(ids)):
+            _, log = run_system(packed[i], lens[i], num_procs=8, cache_size=4, log=True, log_msgs=True,
+                                log_bytes=1 << 26)
+            assert dash.format_events(eng.read_events(i)) == log, ids[i]
+
+
 def test_debug_trace_truncation_is_reported(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4) as eng:

@@ -299,6 +299,22 @@ def test_debug_trace_through_queue_depth_tiers(dash, runs):
             assert dash.format_events(eng.read_events(i)) == log, ids[i]
 
 
+@pytest.mark.parametrize("N,CS,seed", [(1, 3, 0), (3, 16, 0), (5, 5, 0x5EED5EED), (7, 1, 87), (2, 8, 0)])
+def test_debug_trace_other_shapes(dash, N, CS, seed):
+    """The round-major event log of the other kernel instantiations (1..7 nodes, generic and
+    power-of-two cache sizes, lockstep and seeded): every system's log equals the oracle's
+    (tools/diag/event_fuzz.py runs the same check over 512 random configurations)."""
+    rng = np.random.default_rng(31 * N + CS)
+    packed, lens = random_batch(rng, 48, N, 60, block_span=4, hot_frac=0.3)
+    with dash.Engine(48, num_procs=N, cache_size=CS, max_instr=60, trace_events=4096, schedule_seed=seed) as eng:
+        eng.load_traces(packed, lens)
+        eng.run()
+        for s in range(48):
+            _, log = run_system(packed[s], lens[s], num_procs=N, cache_size=CS, log=True, log_msgs=True,
+                                arb_seed=seed)
+            assert dash.format_events(eng.read_events(s)) == log, s
+
+
 def test_debug_trace_truncation_is_reported(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4) as eng:

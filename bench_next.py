@@ -174,9 +174,14 @@ def seeded_row(dash, dev, seed, systems, L, steps):
             digs.append((int((d & np.uint64(0xFFFFFFFF)).sum(dtype=np.uint64)), int((d >> np.uint64(32)).sum(dtype=np.uint64))))
             out[name] = {"instr_per_s": st["instructions"] * steps / el, "ms_per_step": el / steps * 1e3,
                          "kernel_ms": ks, "instructions": st["instructions"], "rounds_total": st["rounds_total"],
-                         "err_systems": st["err_systems"]}
+                         "err_systems": st["err_systems"], "tier_systems": st["tier_systems"],
+                         "wave_rounds": st["wave_rounds"]}
     out["workload"] = f"{systems} systems x 8 nodes x {L} uniform (device generator, seed 0x{seed:X}), schedule seed 0x5EED5EED"
     out["slowdown"] = out["lockstep"]["instr_per_s"] / out["seeded"]["instr_per_s"]
+    # the slowdown split: rounds the schedule needs, and kernel time per wave-round
+    out["rounds_ratio"] = out["seeded"]["rounds_total"] / out["lockstep"]["rounds_total"]
+    out["time_per_wave_round_ratio"] = ((sum(out["seeded"]["kernel_ms"]) / out["seeded"]["wave_rounds"])
+                                        / (sum(out["lockstep"]["kernel_ms"]) / out["lockstep"]["wave_rounds"]))
     out["parity_all_issued"] = out["seeded"]["instructions"] == systems * 8 * L
     out["parity_reproducible"] = digs[1] == digs[2]
     out["differs_from_lockstep"] = digs[0] != digs[1]

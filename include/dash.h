@@ -192,6 +192,18 @@ int dash_generate(dash_t *h, const dash_gen *g);
    the one behind an accepted racy-test output (tests/golden/schedules/). */
 #define DASH_SIT_OUT 0xFFu
 int dash_set_schedule(dash_t *h, const uint8_t *sched, uint32_t rounds);
+/* A micro-step schedule, the finer-grained twin of dash_set_schedule (same handle requirements):
+   acts[r * num_procs + t] = DASH_SIT_OUT, DASH_MICRO_STEP (node t pops or issues, as in a round,
+   and its sends wait in its outbox) or DASH_MICRO_SEND (node t delivers its oldest held message);
+   at most one node acts per round, and every node sits out past `rounds`. This is the
+   reference's own granularity: a thread handles a message, then completes its sendMessage
+   calls (:741-765) one by one while other threads run, so any interleaving of the reference's
+   threads -- e.g. the one the oracle recovers from a reference run's DEBUG logs -- is one such
+   schedule (tests/golden/ref_runs/). A valid schedule never steps a node whose outbox holds
+   messages. Runs at queue depth 256 only (no tiers); pass max_rounds >= the schedule's rounds. */
+#define DASH_MICRO_STEP 0u
+#define DASH_MICRO_SEND 1u
+int dash_set_micro_schedule(dash_t *h, const uint8_t *acts, uint32_t rounds);
 int dash_run(dash_t *h, dash_stats *stats);
 int dash_read_state(dash_t *h, uint64_t sys, dash_node_state *out /* [num_procs] */);
 int dash_read_results(dash_t *h, uint64_t first, uint64_t count, uint64_t *digests,

@@ -1447,9 +1447,32 @@ static int g_succ(const xctx *c, const xguide *g, const xsys *s, uint16_t *st) {
     return n;
 }
 
+static int guided_search(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                         const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
+                         orc_outcome *out, uint64_t *states, int *complete, uint16_t *witness, uint32_t wit_cap,
+                         uint32_t *wit_len);
+
 int orc_guided(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
                const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
                orc_outcome *out, uint64_t *states, int *complete) {
+    return guided_search(cfg, trace, stride, lens, events, ev_count, max_states, found, out, states, complete,
+                         NULL, 0, NULL);
+}
+
+int orc_guided_witness(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                       const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
+                       orc_outcome *out, uint64_t *states, uint16_t *witness, uint32_t wit_cap, uint32_t *wit_len) {
+    int complete = 0;
+    return guided_search(cfg, trace, stride, lens, events, ev_count, max_states, found, out, states, &complete,
+                         witness, wit_cap, wit_len);
+}
+
+/* The DFS keeps each stack entry's depth and the step that made it, so the steps of the path
+   to the state being expanded are path[0 .. depth - 1]: the witness when the logs are met. */
+static int guided_search(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                         const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
+                         orc_outcome *out, uint64_t *states, int *complete, uint16_t *witness, uint32_t wit_cap,
+                         uint32_t *wit_len) {
     xctx c;
     if (cfg->micro != ORC_MICRO_STRICT) return -1;
     if (x_setup(&c, cfg, trace, stride, lens, 0)) return -1;
@@ -1466,14 +1489,31 @@ int orc_guided(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const
     while (vis.cap < max_states + max_states / 2 + 2) vis.cap <<= 1;
     vis.keys = (uint64_t *)calloc(vis.cap, sizeof(uint64_t));
     vis.n = 0;
-    size_t scap = 1024, sn = 0;
+    size_t scap = 1024, sn = 0, pcap = 1024;
     xsys *stack = (xsys *)malloc(sizeof(xsys) * scap);
+    uint32_t *sdepth = (uint32_t *)malloc(sizeof(uint32_t) * scap);
+    uint16_t *sstep = (uint16_t *)malloc(sizeof(uint16_t) * scap);
+    uint16_t *path = (uint16_t *)malloc(sizeof(uint16_t) * pcap);
+    uint32_t hit_depth = 0;
     int rc = 0, full = 1, hit = 0;
-    if (!vis.keys || !stack) { rc = -1; goto done; }
-    x_init(&c, &stack[sn++]);
+    if (!vis.keys || !stack || !sdepth || !sstep || !path) { rc = -1; goto done; }
+    x_init(&c, &stack[sn]);
+    sdepth[sn] = 0;
+    sstep[sn++] = 0;
     xset_insert(&vis, x_hash(&c, &stack[0]));
     while (sn > 0 && !hit) {
-        xsys cur = stack[--sn];
+        --sn;
+        xsys cur = stack[sn];
+        const uint32_t depth = sdepth[sn];
+        if (depth > 0) { /* the path to cur: its parent's path, then the step that made cur */
+            if (depth > pcap) {
+                pcap *= 2;
+                uint16_t *p2 = (uint16_t *)realloc(path, sizeof(uint16_t) * pcap);
+                if (!p2) { rc = -1; break; }
+                path = p2;
+            }
+            path[depth - 1] = sstep[sn];
+        }
         uint16_t succ[4 * ORC_MAX_PROCS];
         const int ns = g_succ(&c, &g, &cur, succ);
         if (ns == 0) {
@@ -1485,6 +1525,7 @@ int orc_guided(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const
                 if (x_enabled(&c, &cur, en) == 0) { /* terminal in the full model too */
                     x_outcome(&c, &cur, out);
                     hit = 1;
+                    hit_depth = depth;
                 }
             }
             continue;
@@ -1498,19 +1539,33 @@ int orc_guided(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const
             if (sn == scap) {
                 scap *= 2;
                 xsys *ns2 = (xsys *)realloc(stack, sizeof(xsys) * scap);
-                if (!ns2) { full = 0; rc = -1; break; }
-                stack = ns2;
+                uint32_t *d2 = ns2 ? (uint32_t *)realloc(sdepth, sizeof(uint32_t) * scap) : NULL;
+                uint16_t *s2 = d2 ? (uint16_t *)realloc(sstep, sizeof(uint16_t) * scap) : NULL;
+                if (ns2) stack = ns2;
+                if (d2) sdepth = d2;
+                if (s2) sstep = s2;
+                if (!ns2 || !d2 || !s2) { full = 0; rc = -1; break; }
             }
-            stack[sn++] = nxt;
+            stack[sn] = nxt;
+            sdepth[sn] = depth + 1;
+            sstep[sn++] = succ[k];
         }
         if (rc) break;
     }
+    if (hit && witness) {
+        for (uint32_t i = 0; i < hit_depth && i < wit_cap; i++) witness[i] = path[i];
+        if (hit_depth > wit_cap) rc = -3;
+    }
+    if (wit_len) *wit_len = hit ? hit_depth : 0;
 done:
     if (found) *found = hit;
     if (states) *states = vis.n;
     if (complete) *complete = hit || (full && rc == 0);
     free(vis.keys);
     free(stack);
+    free(sdepth);
+    free(sstep);
+    free(path);
     free(c.scratch);
     return rc;
 }

@@ -193,6 +193,13 @@ int orc_guided(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const
                const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
                orc_outcome *out, uint64_t *states, int *complete);
 
+/* orc_guided plus the interleaving it found: *wit_len micro-steps (XSTEP: pop / issue / one
+   send of node t), the order in which the reference's threads took them; -3 if more than
+   wit_cap (the witness is then cut). */
+int orc_guided_witness(const orc_cfg *cfg, const uint16_t *trace, uint64_t stride, const uint32_t *lens,
+                       const uint32_t *events, const uint32_t *ev_count, uint64_t max_states, int *found,
+                       orc_outcome *out, uint64_t *states, uint16_t *witness, uint32_t wit_cap, uint32_t *wit_len);
+
 /* An engine round schedule (dash_set_schedule form, [rounds][num_procs]) under which every node
    pops exactly its logged messages and issues where its log says (events as for orc_guided).
    *found = 0 when the search ends without one (the run is not a round-model execution, or the

@@ -1,0 +1,67 @@
+"""Generate tests/golden/ref_runs/micro{4,8}.json: reference runs that are NOT executions of the
+engine's round model, re-enacted through a micro-step schedule (dash_set_micro_schedule).
+
+TEST INFRASTRUCTURE. For the guided pin's traces (tests/ref_pin.py gen_trace_large, seeds in
+order) the reference pin binaries (oracle/_ref/cache_simulator_pin{,8}_cs{1,4}: assignment.c +
+the benchmark patch, -DDEBUG_MSG -DDEBUG_INSTR) run each trace. A run is kept when
+orc_rounds_from_logs proves (complete search) that no engine round schedule reproduces its logs,
+i.e. one of its threads was interleaved between its own sendMessage calls (ref :741-765). The
+oracle's log-guided search (orc_guided_witness, STRICT model) then recovers an interleaving of
+the reference's threads that meets every thread's log: a sequence of micro-steps (a thread pops
+or issues; a thread completes one sendMessage), checked by re-executing it
+(orc_replay_steps: the outcome is the reference's dumps). A case holds the trace, that sequence
+as "P<t>" / "I<t>" (node t pops / issues: a step) and "D<t>" (node t delivers its oldest held
+message) tokens, each
+thread's logged events (ref_pin.log_tokens) and the digest of the reference's dumps.
+
+Run: python tests/golden/make_ref_micro.py   (about a minute)
+"""
+import json
+import pathlib
+import subprocess
+import sys
+import tempfile
+
+HERE = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent))
+import oracle_ctypes as oc  # noqa: E402
+import ref_pin  # noqa: E402
+
+RUNS = 40
+
+
+def main():
+    for n in (4, 8):
+        cases = []
+        seed = 0
+        while len(cases) < RUNS:
+            cs, rows = ref_pin.gen_trace_large(seed, n)
+            tr, lens = ref_pin.as_arrays(rows)
+            with tempfile.TemporaryDirectory() as td:
+                d = pathlib.Path(td)
+                ref_pin.write_trace(d / "tests" / "t", rows)
+                p = subprocess.run(["timeout", "20", str(ref_pin.pin_exe(cs, n)), "t"], cwd=d, capture_output=True,
+                                   text=True, check=True)
+                dumps = [(d / f"core_{k}_output.txt").read_text() for k in range(n)]
+            ev, _ = oc.parse_logs(p.stdout, n)
+            sched, _ = oc.rounds_from_logs(tr, lens, ev, num_procs=n, cache_size=cs, max_states=10_000_000)
+            if sched is None:
+                found, out, steps = oc.guided_witness(tr, lens, ev, num_procs=n, cache_size=cs)
+                digest = oc.dumps_digest(dumps, cs)
+                assert found and out.digest == digest, seed
+                rep, term = oc.replay_steps(tr, lens, steps, num_procs=n, cache_size=cs)
+                assert term and rep.digest == digest, seed
+                acts = " ".join("PID"[int(s) >> 8] + str(int(s) & 15) for s in steps)
+                cases.append({"seed": seed, "num_procs": n, "cache_size": cs,
+                              "trace": [[f"WR 0x{(w >> 8) & 0x7F:02X} {w & 0xFF}" if w & 0x8000 else
+                                         f"RD 0x{(w >> 8) & 0x7F:02X}" for w in r] for r in rows],
+                              "steps": acts, "log": ref_pin.log_tokens(p.stdout, n), "digest": f"{digest:016x}"})
+            seed += 1
+        (HERE / "ref_runs" / f"micro{n}.json").write_text(json.dumps(
+            {"source": f"tests/golden/make_ref_micro.py (oracle/_ref/cache_simulator_pin{'' if n == 4 else n}_cs{{1,4}})",
+             "tried_traces": seed, "cases": cases}, indent=0) + "\n")
+        print(n, "nodes:", len(cases), "non-round-model runs kept of", seed, "traces")
+
+
+if __name__ == "__main__":
+    main()

@@ -92,6 +92,8 @@ def bind(path):
     L.orc_replay_steps.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, I, V, ctypes.c_uint32, V, V]
     L.orc_guided.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, V, U64, V, V, V, V]
     L.orc_guided.restype = ctypes.c_int
+    L.orc_guided_witness.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, V, U64, V, V, V, V, ctypes.c_uint32, V]
+    L.orc_guided_witness.restype = ctypes.c_int
     L.orc_rounds_from_logs.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, V, U64, V, ctypes.c_uint32, V, V, V]
     L.orc_rounds_from_logs.restype = ctypes.c_int
     L.orc_schedule_witness.argtypes = [ctypes.POINTER(OrcCfg), V, U64, V, V, ctypes.c_uint32, V, V]
@@ -352,6 +354,25 @@ def guided(trace, lens, events, num_procs=4, cache_size=4, max_states=2_000_000,
     if rc != 0:
         raise ValueError(f"guided search failed ({rc})")
     return bool(found.value), out, int(states.value), bool(full.value)
+
+
+def guided_witness(trace, lens, events, num_procs=4, cache_size=4, max_states=2_000_000, cap=1 << 16):
+    """orc_guided_witness: (found, outcome, steps uint16) -- the micro-step interleaving (XSTEP
+    words: pop / issue / one send of a node) under which the nodes' logs are met."""
+    trace, lens = _tr(trace, lens)
+    cfg = OrcCfg(num_procs, cache_size, 256, 0, 0, MICRO_STRICT, 0)
+    flat = np.ascontiguousarray([w for e in events for w in e] or [0], dtype=np.uint32)
+    cnt = np.ascontiguousarray([len(e) for e in events], dtype=np.uint32)
+    out = OrcOutcome()
+    found, states, n = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint32()
+    wit = np.zeros(cap, np.uint16)
+    rc = lib().orc_guided_witness(ctypes.byref(cfg), trace.ctypes.data, trace.shape[1], lens.ctypes.data,
+                                  flat.ctypes.data, cnt.ctypes.data, max_states, ctypes.addressof(found),
+                                  ctypes.addressof(out), ctypes.addressof(states), wit.ctypes.data, cap,
+                                  ctypes.addressof(n))
+    if rc != 0:
+        raise ValueError(f"guided witness search failed ({rc})")
+    return bool(found.value), out, wit[:n.value].copy()
 
 
 def rounds_from_logs(trace, lens, events, num_procs=4, cache_size=4, max_states=500_000, cap=4096):

@@ -379,6 +379,26 @@ def replay_cases(n):
         yield c, c["cache_size"], tr, lens, sched
 
 
+def micro_cases(n):
+    """tests/golden/ref_runs/micro{n}.json (make_ref_micro.py): reference runs that are not
+    round-model executions, with the interleaving of the reference's threads the oracle recovered
+    from their logs. Yields (case, cache_size, trace, lens, acts uint8 [rounds][n] in
+    dash_set_micro_schedule form, steps uint16 in the oracle's XSTEP form)."""
+    data = json.loads((oc.ROOT / "tests" / "golden" / "ref_runs" / f"micro{n}.json").read_text())
+    for c in data["cases"]:
+        rows = [[oc.pack(w[0][0], int(w[1], 16), int(w[2]) if len(w) > 2 else 0)
+                 for w in (ln.split() for ln in r)] for r in c["trace"]]
+        tr, lens = as_arrays(rows)
+        toks = c["steps"].split()
+        acts = np.full((len(toks), n), 0xFF, np.uint8)
+        steps = np.zeros(len(toks), np.uint16)
+        for r, tk in enumerate(toks):
+            t = int(tk[1:])
+            acts[r, t] = 1 if tk[0] == "D" else 0  # MICRO_SEND / MICRO_STEP (a pop or an issue)
+            steps[r] = "PID".index(tk[0]) << 8 | t  # the oracle's XSTEP: pop / issue / send
+        yield c, c["cache_size"], tr, lens, acts, steps
+
+
 def log_tokens(text, n):
     """Each thread's DEBUG_MSG / DEBUG_INSTR lines (ref :179-182, :649-652) as tokens, in the
     thread's order: pops "type.sender.ADDR", issues "R.ADDR" / "W.ADDR.value"."""

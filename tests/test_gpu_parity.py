@@ -534,6 +534,47 @@ def test_engine_reenacts_reference_runs(dash, n):
     assert k == 40
 
 
+@pytest.mark.parametrize("n", [4, 8])
+def test_engine_reenacts_non_round_model_runs(dash, n):
+    """The reference runs the round model cannot express (tests/golden/ref_runs/micro{n}.json: a
+    thread interleaved between its own sendMessage calls, 40 per node count): driven through the
+    interleaving the oracle recovered from each run's logs, as a micro-step schedule
+    (dash_set_micro_schedule, sim_kernel MODE 4: steps hold their sends in an LDS outbox, sends
+    are delivered one per round), the engine's event log equals the reference's DEBUG_MSG /
+    DEBUG_INSTR lines thread by thread, and its final state is the reference's dumps (digest)."""
+    import ref_pin
+    k = 0
+    for c, cs, tr, lens, acts, _ in ref_pin.micro_cases(n):
+        with dash.Engine(1, num_procs=n, cache_size=cs, max_instr=32, trace_events=4096, schedule_seed=1) as eng:
+            eng.set_micro_schedule(acts)
+            eng.load_traces(tr[None], lens[None])
+            st = eng.run()
+            dig = int(eng.read_results()[0][0])
+            ev = eng.read_events(0)
+        assert not st["err_bits"] & (dash.ERR_ROUNDCAP | dash.ERR_DEADLOCK), c["seed"]  # the schedule ran to quiescence
+        assert dig == int(c["digest"], 16), c["seed"]
+        got = ref_pin.event_tokens([(e.node, e.kind == dash.EV_INSTR, e.word) for e in ev], n)
+        assert got == c["log"], c["seed"]
+        k += 1
+    assert k == 40
+
+
+def test_set_micro_schedule_checks_its_input(dash):
+    tr, lens = load_test_dir(GOLDEN / "test_4")
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, schedule_seed=1) as eng:
+        two = np.full((3, 4), dash.SIT_OUT, np.uint8)
+        two[1, 0] = two[1, 2] = dash.MICRO_STEP
+        with pytest.raises(dash.DashError):
+            eng.set_micro_schedule(two)
+        bad = np.full((3, 4), dash.SIT_OUT, np.uint8)
+        bad[0, 1] = 5
+        with pytest.raises(dash.DashError):
+            eng.set_micro_schedule(bad)
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32) as eng:
+        with pytest.raises(dash.DashError):
+            eng.set_micro_schedule(np.full((2, 4), dash.SIT_OUT, np.uint8))
+
+
 def test_set_schedule_checks_its_input(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32) as eng:

@@ -128,3 +128,22 @@ def test_reference_runs_replay_on_the_round_model(n):
         assert ref_pin.log_tokens(log, n) == c["log"], c["seed"]
         k += 1
     assert k == 40
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_reference_runs_replay_as_micro_steps(n):
+    """Reference runs that are NOT executions of the engine's round model (tests/golden/ref_runs/
+    micro{n}.json, make_ref_micro.py: a complete search found no round schedule for their logs --
+    a thread was interleaved between its own sendMessage calls): the interleaving of the
+    reference's threads that the oracle recovered from each run's logs, re-executed micro-step by
+    micro-step (pop / issue / one send), ends quiescent in the reference's dumps (digest).
+    tests/test_gpu_parity.py drives the engine through the same interleavings
+    (dash_set_micro_schedule)."""
+    k = 0
+    for c, cs, tr, lens, acts, steps in ref_pin.micro_cases(n):
+        out, terminal = oc.replay_steps(tr, lens, steps, num_procs=n, cache_size=cs)
+        assert terminal and out.digest == int(c["digest"], 16), c["seed"]
+        assert (acts != 0xFF).sum(axis=1).max() == 1  # one acting node per round
+        k += 1
+    assert k == 40
+

@@ -41,6 +41,7 @@ struct dash_ctx {
     uint32_t* d_events = nullptr;       // [sys][round / 4][node][round % 4] (rounds: ev_rounds)
     uint32_t* d_arb = nullptr;          // seeded schedule: one word per node and round (dash::arb_node)
     uint32_t arb_len = 0;
+    bool micro = false;                 // the round table is a micro-step schedule (MODE 4)
     uint32_t* d_event_count = nullptr;  // [sys*N+node]
     uint32_t ev_rounds = 0;             // trace_events rounded up to a multiple of 4
     uint64_t tier_systems[dash::NUM_TIERS] = {};  // systems run per queue-depth tier, last run
@@ -381,6 +382,46 @@ int dash_set_schedule(dash_t* h, const uint8_t* sched, uint32_t rounds) {
         HIPCHK(h, hipMemcpyAsync(h->d_arb, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         h->ran = false;
+        h->micro = false;
+        return DASH_OK;
+    });
+}
+
+int dash_set_micro_schedule(dash_t* h, const uint8_t* acts, uint32_t rounds) {
+    return guarded(h, "dash_set_micro_schedule", [&]() -> int {
+        if (!h || (!acts && rounds)) return DASH_EINVAL;
+        if (!h->d_arb) return fail(h, DASH_ESTATE, "dash_set_micro_schedule: handle created with schedule_seed = 0");
+        const uint32_t N = h->cfg.num_procs, P = h->seg;
+        if (h->arb_len < h->cfg.max_rounds)
+            return fail(h, DASH_EINVAL, "dash_set_micro_schedule: the round table holds %u of max_rounds %llu rounds",
+                        h->arb_len, (unsigned long long)h->cfg.max_rounds);
+        if (rounds > h->arb_len)
+            return fail(h, DASH_EINVAL, "dash_set_micro_schedule: %u rounds > max_rounds", rounds);
+        for (uint32_t r = 0; r < rounds; r++) {
+            uint32_t acting = 0;
+            for (uint32_t t = 0; t < N; t++) {
+                const uint8_t v = acts[(uint64_t)r * N + t];
+                if (v == DASH_SIT_OUT) continue;
+                if (v != DASH_MICRO_STEP && v != DASH_MICRO_SEND)
+                    return fail(h, DASH_EINVAL, "dash_set_micro_schedule: round %u node %u: action %u invalid", r, t,
+                                (unsigned)v);
+                ++acting;
+            }
+            if (acting > 1) return fail(h, DASH_EINVAL, "dash_set_micro_schedule: round %u: %u nodes act", r, acting);
+        }
+        // table words (dash_kernels.hip MODE 4): 0 = sits out, 1 = steps, 2 = sends one held
+        // message; every node sits out past the schedule
+        std::vector<uint32_t> tab(((uint64_t)h->arb_len + 4) * P, 0);
+        for (uint64_t r = 0; r < rounds; r++)
+            for (uint32_t t = 0; t < N; t++) {
+                const uint8_t v = acts[r * N + t];
+                tab[((r >> 2) * P + t) * 4 + (r & 3)] = v == DASH_SIT_OUT ? 0u : v == DASH_MICRO_STEP ? 1u : 2u;
+            }
+        HIPCHK(h, hipSetDevice(h->cfg.device));
+        HIPCHK(h, hipMemcpyAsync(h->d_arb, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->ran = false;
+        h->micro = true;
         return DASH_OK;
     });
 }
@@ -405,6 +446,7 @@ int dash_run(dash_t* h, dash_stats* stats) {
     a.arb_seed = h->cfg.schedule_seed;
     a.arb_tab = h->d_arb;
     a.arb_len = h->arb_len;
+    a.micro = h->micro ? 1u : 0u;
     a.cache_size = h->cfg.cache_size;
     for (uint32_t b = 0; b < 16; b++)  // b % CACHE_SIZE for the generic (non-power-of-two) kernels
         a.cs_lut |= (uint64_t)(b % h->cfg.cache_size) << (4 * b);
@@ -423,7 +465,8 @@ int dash_run(dash_t* h, dash_stats* stats) {
     uint64_t todo = h->cfg.num_systems;
     const uint32_t* list = nullptr;
     const uint32_t f = h->cfg.flags;
-    const int first = (f & DASH_TIER_FROM_256) ? 2 : (f & DASH_TIER_FROM_32) ? 1 : h->auto_tier;
+    // a micro-step schedule runs at the reference's queue depth only (sim_kernel MODE 4)
+    const int first = (h->micro || (f & DASH_TIER_FROM_256)) ? 2 : (f & DASH_TIER_FROM_32) ? 1 : h->auto_tier;
     if (h->hint_n && h->hint_tier != first) HIPCHK(h, reset_hint(h));
     // Systems that overflowed the first tier in an earlier run of these traces (the
     // schedule is deterministic, so they will again) start one tier deeper on the side

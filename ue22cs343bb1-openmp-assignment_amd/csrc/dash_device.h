@@ -53,6 +53,7 @@ struct SimArgs {
     uint64_t arb_seed;        // 0: lowest-sender-first lockstep; else the seeded schedule
     const uint32_t* arb_tab;  // seeded schedule: per-round word (arb_word) for rounds < arb_len
     uint32_t arb_len;         // a multiple of 4; rounds beyond it hash their key in the kernel
+    uint32_t micro;           // 1: arb_tab is a micro-step table (dash_set_micro_schedule, MODE 4)
     const uint8_t* skip;      // optional [sys]: 1 = run elsewhere this pass (a deeper tier, concurrently)
     uint32_t cache_size;      // CACHE_SIZE (ref :7); read by the generic (non-power-of-two) kernels
     uint64_t cs_lut;          // nibble b = b % cache_size, b < 16 (generic kernels)

@@ -47,6 +47,7 @@ enum : uint32_t { D_EM = 0, D_S = 1, D_U = 2 };              // directoryEntrySt
 #ifndef DASH_WCHUNK
 #define DASH_WCHUNK 4
 #endif
+constexpr uint32_t OUTBOX = 8;  // MODE 4: held sends per node (one step: at most 7 INVs + one notice)
 constexpr uint32_t WIN = 2;        // trace window chunks per lane (enough: see the refill)
 constexpr uint32_t CHUNK = CHUNK_INSTR;   // instructions per 8-B HBM trace chunk (layout unit)
 constexpr uint32_t WCHUNK = DASH_WCHUNK;  // instructions per window refill (2: 4-B, 4: 8-B loads)
@@ -165,7 +166,11 @@ __device__ __forceinline__ mask_t Mbit15(uint32_t v) {
 //       with probability 1/4 and senders deliver in a seeded affine order; oracle twins
 //       orc_arb_stall, orc_arb_prio);
 //   2 = the DEBUG_MSG / DEBUG_INSTR event log (a.events) under lockstep;
-//   3 = the event log under a seeded (or explicit) schedule.
+//   3 = the event log under a seeded (or explicit) schedule;
+//   4 = an explicit micro-step schedule with the event log (a.micro, dash_set_micro_schedule): per
+//       round one node either steps, holding its sends in an LDS outbox, or delivers its oldest
+//       held message -- the reference's threads interleaved at sendMessage granularity, as in
+//       the oracle's STRICT model (queue depth 256 only).
 // Mode 1 without the event-log code keeps its loop free of SGPR spill reloads; the schedule is a
 // compile-time property of every mode (a run-time test in the event-log kernel cost it 12 %).
 template <int P, int CS, uint32_t RING, int MODE>
@@ -175,13 +180,15 @@ __attribute__((amdgpu_waves_per_eu(DASH_WAVES_PER_EU)))
 #endif
 void sim_kernel(const SimArgs a) {
     constexpr bool SLOW = MODE != 0;
-    constexpr bool ARB = MODE == 1 || MODE == 3;  // the seeded / explicit schedule is on
+    constexpr bool MICRO = MODE == 4;              // an explicit micro-step schedule (held sends)
+    constexpr bool ARB = MODE == 1 || MODE == 3 || MICRO;  // the seeded / explicit schedule is on
     constexpr bool EVLOG = MODE >= 2;              // the DEBUG event log is on
     using L = Lds<P, CS, RING>;
     const uint32_t ncs = CS ? (uint32_t)CS : a.cache_size;  // cache lines per node
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;
-    __shared__ __attribute__((aligned(16))) uint32_t lds[L::WORDS];
+    // MODE 4 adds each node's outbox: 8 entries of (message word, receiver) after the common area
+    __shared__ __attribute__((aligned(16))) uint32_t lds[MICRO ? L::WORDS + OUTBOX * 128 : L::WORDS];
     uint16_t* const lds16 = reinterpret_cast<uint16_t*>(lds);
 
     const uint32_t lane = threadIdx.x;
@@ -276,6 +283,11 @@ void sim_kernel(const SimArgs a) {
     uint32_t last_act = ~0u;  // last round this node was active (rounds = max over the system + 1)
     uint32_t nev = 0;         // events logged (DEBUG_MSG / DEBUG_INSTR emission, off unless a.events)
     uint32_t ev0 = 0, ev1 = 0, ev2 = 0, ev3 = 0;  // this node's log words of the current four rounds (MODE 2, 3)
+    uint32_t oh = 0, on = 0;  // MODE 4: this node's outbox head and count
+    auto held = [&]() -> mask_t {
+        if constexpr (MICRO) return M(on != 0u);
+        else return 0;
+    };
     // loop-invariant uniform values a round needs, kept in VGPRs: the round's lane masks
     // need the SGPRs (spilling them costs VALU)
     // rcv_all: the nodes a REPLY_ID fan-out reaches (every node of the system but this one:
@@ -357,7 +369,7 @@ void sim_kernel(const SimArgs a) {
     auto step = [&](const uint32_t k, const mask_t mMsg, const mask_t mIss) __attribute__((always_inline)) {
         // A system is active while any of its nodes has a message or can issue;
         // quiescence is absorbing, so the active rounds of a system are 0..R-1.
-        last_act = B(mMsg | mIss) ? rv + k : last_act;
+        last_act = B(mMsg | mIss | held()) ? rv + k : last_act;
         // ---- one step: pop one message (ref :167-177) or issue one instruction (ref :632-647) ----
         mask_t mStall = 0;
         uint32_t bitI = 1u << (4 * t);
@@ -367,8 +379,13 @@ void sim_kernel(const SimArgs a) {
             // the trip start past the table's end; 0 = the node sits the round out, else its
             // primary arrival bit
             wp = k == 0 ? arbw.x : k == 1 ? arbw.y : k == 2 ? arbw.z : arbw.w;
-            mStall = M(wp == 0u);
-            bitI = wp >> 1;
+            if constexpr (MICRO) {  // 1: the node steps (its sends are held), 2: it sends one held message
+                mStall = M(wp != 1u);
+                bitI = 1u;
+            } else {
+                mStall = M(wp == 0u);
+                bitI = wp >> 1;
+            }
         }
         const mask_t mHas = mMsg & ~mStall;           // pops this round
         const mask_t mDo = mIss & ~mMsg & ~mStall;    // issues this round
@@ -558,14 +575,48 @@ void sim_kernel(const SimArgs a) {
         // compares the receiver's count plus that rank with the ring depth.
         // tail (with ring column); the final tier adds count << 16 for the capacity check
         lds[L::MQT + L::MQS * lane] = FINAL ? tq | (cq << 8) : tq;
+        // MODE 4 (micro-step schedule, dash_set_micro_schedule): the step's sends go to this
+        // node's outbox in program order -- the INVs in ascending receiver order, then the
+        // reply, forward or eviction notice, then the flush copy (ref :364-379, :281, :498) --
+        // and a node whose word is 2 delivers the first one; one node acts per round, so every
+        // delivery is the only arrival at its receiver
+        mask_t xVP = mVP, xVB = mVB, xRID = mRID;
+        uint32_t xdP = dP, xwP = wP;
+        if constexpr (MICRO) {
+            auto push = [&](uint32_t w, uint32_t d) {
+                const uint32_t e = L::WORDS + ((oh + on) & (OUTBOX - 1u)) * 128u + lane;
+                lds[e] = w;
+                lds[e + 64] = d;
+                ++on;
+            };
+            if (B(mRID)) {
+                const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
+                for (uint32_t im = mv16 & rcv_all; im != 0; im &= im - 1u) push(winv, (uint32_t)__builtin_ctz(im));
+            }
+            if (B(mVP)) push(wP, dP);
+            if (B(mVB)) push(wA, msr);
+            const bool snd = wp == 2u && on != 0u;
+            xdP = lds[L::WORDS + oh * 128u + 64 + lane];
+            xwP = lds[L::WORDS + oh * 128u + lane];
+            oh = snd ? (oh + 1u) & (OUTBOX - 1u) : oh;
+            on -= snd ? 1u : 0u;
+            xVP = M(snd);
+            xVB = 0;
+            xRID = 0;
+        }
         uint32_t bitP = bitI << 1, bitB = bitI << 2;
         if (ARB) {
-            bitP = wp;
-            bitB = dbl(wp);
+            if constexpr (MICRO) {  // the round's only arrival at its receiver
+                bitP = 2u;
+                bitB = 4u;
+            } else {
+                bitP = wp;
+                bitB = dbl(wp);
+            }
         }
-        if (B(mVP))
-            __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + dP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (B(mVB))
+        if (B(xVP))
+            __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + xdP)], bitP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (B(xVB))
             __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + msr)], bitB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         auto place = [&](mask_t v, uint32_t d, uint32_t bit, uint32_t w) {
             const uint32_t rcv = L::MQS * (seg + d);
@@ -591,21 +642,21 @@ void sim_kernel(const SimArgs a) {
         // test: its arrival bits, then its ring stores. The primary and flush-copy bits are
         // already set above, so these ranks see every arrival of the round; the places below
         // read the masks after the INV bits too.
-        if (mRID != 0) {
+        if (xRID != 0) {
             COLD();
-            if (B(mRID)) {
+            if (B(xRID)) {
                 for (uint32_t im = mv16 & rcv_all; im != 0; im &= im - 1u)
                     __hip_atomic_fetch_or(&lds[L::MQM + L::MQS * (seg + (uint32_t)__builtin_ctz(im))], bitI,
                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            if (B(mRID)) {
+            if (B(xRID)) {
                 const uint32_t winv = mk(T_INV, t, addr, 0, 0, 0);
                 for (uint32_t im = mv16 & rcv_all; im != 0; im &= im - 1u)
                     place(M(true), (uint32_t)__builtin_ctz(im), bitI, winv);
             }
         }
-        place(mVP, dP, bitP, wP);
-        place(mVB, msr, bitB, wA);
+        place(xVP, xdP, bitP, xwP);
+        place(xVB, msr, bitB, wA);
         const uint32_t arrived = __hip_atomic_exchange(&lds[L::MQM + L::MQS * lane], 0u, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         uint32_t n = (uint32_t)__builtin_popcount(arrived) << 8;
@@ -675,7 +726,7 @@ void sim_kernel(const SimArgs a) {
     mask_t mMsg = can_pop(), mIss = can_issue();
     // quiescence is absorbing, so testing it once per trip only adds idle rounds (no
     // state changes, not counted in `rounds`)
-    while ((mMsg | mIss) != 0) {
+    while ((mMsg | mIss | held()) != 0) {
         cap_check(rv, mMsg, mIss);
         // a non-final tier stops a system soon after its first overflow: it will be
         // re-simulated from scratch at the next depth, its results here are void
@@ -700,10 +751,15 @@ void sim_kernel(const SimArgs a) {
             if (rv + 4 < a.arb_len) arbn = arbt[((rv + 4) >> 2) * P];
             if (rv >= a.arb_len) {  // past the table (arb_len is a multiple of 4, like rv)
                 COLD();
-                const uint32_t r0 = __builtin_amdgcn_readfirstlane(rv);
-                arbw = make_uint4(arb_node(arb_word(a.arb_seed, r0, P), t), arb_node(arb_word(a.arb_seed, r0 + 1, P), t),
-                                  arb_node(arb_word(a.arb_seed, r0 + 2, P), t),
-                                  arb_node(arb_word(a.arb_seed, r0 + 3, P), t));
+                if constexpr (MICRO) {  // past a micro-step table every node sits out
+                    arbw = make_uint4(0, 0, 0, 0);
+                } else {
+                    const uint32_t r0 = __builtin_amdgcn_readfirstlane(rv);
+                    arbw = make_uint4(arb_node(arb_word(a.arb_seed, r0, P), t),
+                                      arb_node(arb_word(a.arb_seed, r0 + 1, P), t),
+                                      arb_node(arb_word(a.arb_seed, r0 + 2, P), t),
+                                      arb_node(arb_word(a.arb_seed, r0 + 3, P), t));
+                }
             }
         }
         step(0, mMsg, mIss);
@@ -875,7 +931,12 @@ __global__ __launch_bounds__(256) void gen_kernel(const GenArgs g) {
 
 template <int P, int CS, uint32_t RING>
 static hipError_t launch_sim_pcr(const SimArgs& a, uint64_t groups, hipStream_t s) {
-    if (a.events && a.arb_seed)
+    if (a.micro) {  // micro-step schedules run at the reference's queue depth only
+        if constexpr (RING == 256)
+            hipLaunchKernelGGL((sim_kernel<P, CS, RING, 4>), dim3((uint32_t)groups), dim3(64), 0, s, a);
+        else
+            return hipErrorInvalidValue;
+    } else if (a.events && a.arb_seed)
         hipLaunchKernelGGL((sim_kernel<P, CS, RING, 3>), dim3((uint32_t)groups), dim3(64), 0, s, a);
     else if (a.events)
         hipLaunchKernelGGL((sim_kernel<P, CS, RING, 2>), dim3((uint32_t)groups), dim3(64), 0, s, a);

@@ -52,8 +52,10 @@ EXPORTS = ("dash_create", "dash_destroy", "dash_last_error", "dash_load_traces",
            "dash_parse_core_file", "dash_resolve_dir", "dash_load_dir", "dash_init_node_state",
            "dash_dump_node", "dash_dump_file", "dash_digest_node", "dash_simulate_dir",
            "dash_read_events", "dash_format_event", "dash_load_dirs", "dash_dump_system",
-           "dash_write_digests", "dash_run_host_batched", "dash_set_schedule", "dash_probe_box")
+           "dash_write_digests", "dash_run_host_batched", "dash_set_schedule", "dash_probe_box",
+           "dash_set_micro_schedule")
 SIT_OUT = 0xFF
+MICRO_STEP, MICRO_SEND = 0, 1  # dash_set_micro_schedule actions
 
 
 class DashError(RuntimeError):
@@ -137,6 +139,7 @@ def lib() -> ctypes.CDLL:
         "dash_load_traces": (i32, [vp, vp, u64, vp, u64]),
         "dash_generate": (i32, [vp, ctypes.POINTER(Gen)]),
         "dash_set_schedule": (i32, [vp, vp, u32]),
+        "dash_set_micro_schedule": (i32, [vp, vp, u32]),
         "dash_probe_box": (i32, [i32, ctypes.POINTER(BoxProbe)]),
         "dash_run": (i32, [vp, ctypes.POINTER(Stats)]),
         "dash_read_state": (i32, [vp, u64, ctypes.POINTER(NodeState)]),
@@ -327,6 +330,14 @@ class Engine:
         sched = np.ascontiguousarray(sched, dtype=np.uint8)
         assert sched.ndim == 2 and sched.shape[1] == self.num_procs
         _check(lib().dash_set_schedule(self.h, sched.ctypes.data, sched.shape[0]), "dash_set_schedule", self.h)
+
+    def set_micro_schedule(self, acts: np.ndarray):
+        """dash_set_micro_schedule: uint8 [rounds][num_procs] of SIT_OUT / MICRO_STEP / MICRO_SEND,
+        at most one acting node per round (include/dash.h). Needs schedule_seed != 0."""
+        acts = np.ascontiguousarray(acts, dtype=np.uint8)
+        assert acts.ndim == 2 and acts.shape[1] == self.num_procs
+        _check(lib().dash_set_micro_schedule(self.h, acts.ctypes.data, acts.shape[0]), "dash_set_micro_schedule",
+               self.h)
 
     def run(self) -> dict:
         st = Stats()

@@ -14,7 +14,8 @@ as "P<t>" / "I<t>" (node t pops / issues: a step) and "D<t>" (node t delivers it
 message) tokens, each
 thread's logged events (ref_pin.log_tokens) and the digest of the reference's dumps.
 
-Run: python tests/golden/make_ref_micro.py   (about a minute)
+Run: python tests/golden/make_ref_micro.py [--all]   (about a minute; --all writes ref_runs/all{4,8}.json:
+one run of each of the first ALL traces, none selected)
 """
 import json
 import pathlib
@@ -28,34 +29,63 @@ import oracle_ctypes as oc  # noqa: E402
 import ref_pin  # noqa: E402
 
 RUNS = 40
+ALL = 160  # consecutive traces per node count for ref_runs/all{n}.json: every run kept, none selected
+
+
+def case_of(seed, n, only_non_round):
+    """One reference run of trace `seed` as a micro-step case, or None when only_non_round and a
+    round schedule exists for it."""
+    cs, rows = ref_pin.gen_trace_large(seed, n)
+    tr, lens = ref_pin.as_arrays(rows)
+    with tempfile.TemporaryDirectory() as td:
+        d = pathlib.Path(td)
+        ref_pin.write_trace(d / "tests" / "t", rows)
+        p = subprocess.run(["timeout", "20", str(ref_pin.pin_exe(cs, n)), "t"], cwd=d, capture_output=True,
+                           text=True, check=True)
+        dumps = [(d / f"core_{k}_output.txt").read_text() for k in range(n)]
+    ev, _ = oc.parse_logs(p.stdout, n)
+    round_model = None
+    if only_non_round:
+        sched, _ = oc.rounds_from_logs(tr, lens, ev, num_procs=n, cache_size=cs, max_states=10_000_000)
+        if sched is not None:
+            return None
+        round_model = False
+    found, out, steps = oc.guided_witness(tr, lens, ev, num_procs=n, cache_size=cs)
+    digest = oc.dumps_digest(dumps, cs)
+    assert found and out.digest == digest, seed
+    rep, term = oc.replay_steps(tr, lens, steps, num_procs=n, cache_size=cs)
+    assert term and rep.digest == digest, seed
+    c = {"seed": seed, "num_procs": n, "cache_size": cs,
+         "trace": [[f"WR 0x{(w >> 8) & 0x7F:02X} {w & 0xFF}" if w & 0x8000 else f"RD 0x{(w >> 8) & 0x7F:02X}"
+                    for w in r] for r in rows],
+         "steps": " ".join("PID"[int(x) >> 8] + str(int(x) & 15) for x in steps),
+         "log": ref_pin.log_tokens(p.stdout, n), "digest": f"{digest:016x}"}
+    if round_model is not None:
+        c["round_model"] = round_model
+    return c
+
+
+def main_all():
+    """ref_runs/all{n}.json: one reference run of each of the first ALL traces, every one kept."""
+    for n in (4, 8):
+        cases = [case_of(seed, n, False) for seed in range(ALL)]
+        (HERE / "ref_runs" / f"all{n}.json").write_text(json.dumps(
+            {"source": f"tests/golden/make_ref_micro.py --all (oracle/_ref/cache_simulator_pin{'' if n == 4 else n}_cs{{1,4}})",
+             "traces": ALL, "cases": cases}, separators=(",", ":")) + "\n")
+        print(n, "nodes:", len(cases), "runs, every one kept")
 
 
 def main():
+    if "--all" in sys.argv:
+        return main_all()
     for n in (4, 8):
         cases = []
         seed = 0
         while len(cases) < RUNS:
-            cs, rows = ref_pin.gen_trace_large(seed, n)
-            tr, lens = ref_pin.as_arrays(rows)
-            with tempfile.TemporaryDirectory() as td:
-                d = pathlib.Path(td)
-                ref_pin.write_trace(d / "tests" / "t", rows)
-                p = subprocess.run(["timeout", "20", str(ref_pin.pin_exe(cs, n)), "t"], cwd=d, capture_output=True,
-                                   text=True, check=True)
-                dumps = [(d / f"core_{k}_output.txt").read_text() for k in range(n)]
-            ev, _ = oc.parse_logs(p.stdout, n)
-            sched, _ = oc.rounds_from_logs(tr, lens, ev, num_procs=n, cache_size=cs, max_states=10_000_000)
-            if sched is None:
-                found, out, steps = oc.guided_witness(tr, lens, ev, num_procs=n, cache_size=cs)
-                digest = oc.dumps_digest(dumps, cs)
-                assert found and out.digest == digest, seed
-                rep, term = oc.replay_steps(tr, lens, steps, num_procs=n, cache_size=cs)
-                assert term and rep.digest == digest, seed
-                acts = " ".join("PID"[int(s) >> 8] + str(int(s) & 15) for s in steps)
-                cases.append({"seed": seed, "num_procs": n, "cache_size": cs,
-                              "trace": [[f"WR 0x{(w >> 8) & 0x7F:02X} {w & 0xFF}" if w & 0x8000 else
-                                         f"RD 0x{(w >> 8) & 0x7F:02X}" for w in r] for r in rows],
-                              "steps": acts, "log": ref_pin.log_tokens(p.stdout, n), "digest": f"{digest:016x}"})
+            c = case_of(seed, n, True)
+            if c is not None:
+                del c["round_model"]
+                cases.append(c)
             seed += 1
         (HERE / "ref_runs" / f"micro{n}.json").write_text(json.dumps(
             {"source": f"tests/golden/make_ref_micro.py (oracle/_ref/cache_simulator_pin{'' if n == 4 else n}_cs{{1,4}})",

@@ -379,12 +379,13 @@ def replay_cases(n):
         yield c, c["cache_size"], tr, lens, sched
 
 
-def micro_cases(n):
+def micro_cases(n, name="micro"):
     """tests/golden/ref_runs/micro{n}.json (make_ref_micro.py): reference runs that are not
-    round-model executions, with the interleaving of the reference's threads the oracle recovered
+    round-model executions (name "all": one run of each of the first 160 traces, none selected),
+    with the interleaving of the reference's threads the oracle recovered
     from their logs. Yields (case, cache_size, trace, lens, acts uint8 [rounds][n] in
     dash_set_micro_schedule form, steps uint16 in the oracle's XSTEP form)."""
-    data = json.loads((oc.ROOT / "tests" / "golden" / "ref_runs" / f"micro{n}.json").read_text())
+    data = json.loads((oc.ROOT / "tests" / "golden" / "ref_runs" / f"{name}{n}.json").read_text())
     for c in data["cases"]:
         rows = [[oc.pack(w[0][0], int(w[1], 16), int(w[2]) if len(w) > 2 else 0)
                  for w in (ln.split() for ln in r)] for r in c["trace"]]

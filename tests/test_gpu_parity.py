@@ -496,6 +496,28 @@ def test_cli_round_schedule_file(dash, tmp_path):
                 (GOLDEN / "test_4" / run / f"core_{n}_output.txt").read_bytes(), (run, n)
 
 
+@pytest.mark.parametrize("n", [4, 8])
+def test_cli_micro_schedule_file(dash, n, tmp_path):
+    """`cache_simulator DIR --micro CASE.json --debug-instr --debug-msg`: the drop-in CLI driven by
+    a micro-step schedule prints the reference run's DEBUG lines (thread by thread) and writes its
+    dumps, for the first non-round-model reference runs of tests/golden/ref_runs/micro{n}.json."""
+    import ref_pin
+    exe = dash.PKG / "cache_simulator"
+    for i, (c, cs, tr, lens, acts, _) in enumerate(ref_pin.micro_cases(n)):
+        if i == 4:
+            break
+        d = tmp_path / str(i)
+        rows = [[tr[t, j] for j in range(lens[t])] for t in range(n)]
+        ref_pin.write_trace(d / "tests" / "t", rows)
+        (d / "case.json").write_text(json.dumps(c))
+        p = subprocess.run([str(exe), "t", "-n", str(n), "-c", str(cs), "--micro", "case.json", "--debug-instr",
+                            "--debug-msg"], cwd=d, capture_output=True, text=True, timeout=120)
+        assert p.returncode in (0, 2), p.stderr  # 2: a reference UB flag, reported as in any run
+        assert ref_pin.log_tokens(p.stdout, n) == c["log"], c["seed"]
+        dumps = [(d / f"core_{k}_output.txt").read_text() for k in range(n)]
+        assert oracle_ctypes.dumps_digest(dumps, cs) == int(c["digest"], 16), c["seed"]
+
+
 @pytest.mark.parametrize("N,CS", [(8, 4), (5, 2), (4, 1)])
 def test_explicit_schedule_bit_exact(dash, N, CS):
     """dash_set_schedule with random round tables (each node sits a round out with its own
@@ -534,6 +556,33 @@ def test_engine_reenacts_reference_runs(dash, n):
     assert k == 40
 
 
+def reenact_micro(dash, n, name):
+    import ref_pin
+    k = 0
+    for c, cs, tr, lens, acts, _ in ref_pin.micro_cases(n, name):
+        with dash.Engine(1, num_procs=n, cache_size=cs, max_instr=32, trace_events=4096, schedule_seed=1) as eng:
+            eng.set_micro_schedule(acts)
+            eng.load_traces(tr[None], lens[None])
+            st = eng.run()
+            dig = int(eng.read_results()[0][0])
+            ev = eng.read_events(0)
+        assert not st["err_bits"] & (dash.ERR_ROUNDCAP | dash.ERR_DEADLOCK), c["seed"]  # ran to quiescence
+        assert dig == int(c["digest"], 16), c["seed"]
+        got = ref_pin.event_tokens([(e.node, e.kind == dash.EV_INSTR, e.word) for e in ev], n)
+        assert got == c["log"], c["seed"]
+        k += 1
+    return k
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_engine_reenacts_every_logged_reference_run(dash, n):
+    """No selection: one reference run of each of the first 160 guided-pin traces per node count
+    (tests/golden/ref_runs/all{n}.json), round-model executions or not, re-enacted through the
+    micro-step schedule the oracle recovered from its logs: the engine's event log equals the
+    reference's thread by thread and its final state equals the reference's dumps, every run."""
+    assert reenact_micro(dash, n, "all") == 160
+
+
 @pytest.mark.parametrize("n", [4, 8])
 def test_engine_reenacts_non_round_model_runs(dash, n):
     """The reference runs the round model cannot express (tests/golden/ref_runs/micro{n}.json: a
@@ -542,21 +591,7 @@ def test_engine_reenacts_non_round_model_runs(dash, n):
     (dash_set_micro_schedule, sim_kernel MODE 4: steps hold their sends in an LDS outbox, sends
     are delivered one per round), the engine's event log equals the reference's DEBUG_MSG /
     DEBUG_INSTR lines thread by thread, and its final state is the reference's dumps (digest)."""
-    import ref_pin
-    k = 0
-    for c, cs, tr, lens, acts, _ in ref_pin.micro_cases(n):
-        with dash.Engine(1, num_procs=n, cache_size=cs, max_instr=32, trace_events=4096, schedule_seed=1) as eng:
-            eng.set_micro_schedule(acts)
-            eng.load_traces(tr[None], lens[None])
-            st = eng.run()
-            dig = int(eng.read_results()[0][0])
-            ev = eng.read_events(0)
-        assert not st["err_bits"] & (dash.ERR_ROUNDCAP | dash.ERR_DEADLOCK), c["seed"]  # the schedule ran to quiescence
-        assert dig == int(c["digest"], 16), c["seed"]
-        got = ref_pin.event_tokens([(e.node, e.kind == dash.EV_INSTR, e.word) for e in ev], n)
-        assert got == c["log"], c["seed"]
-        k += 1
-    assert k == 40
+    assert reenact_micro(dash, n, "micro") == 40
 
 
 def test_set_micro_schedule_checks_its_input(dash):

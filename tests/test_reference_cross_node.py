@@ -147,3 +147,16 @@ def test_reference_runs_replay_as_micro_steps(n):
         k += 1
     assert k == 40
 
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_every_logged_reference_run_replays_as_micro_steps(n):
+    """No selection: one reference run of each of the first 160 guided-pin traces per node count
+    (tests/golden/ref_runs/all{n}.json, make_ref_micro.py --all), round-model executions or not,
+    replays micro-step by micro-step on the oracle into the reference's dumps."""
+    k = 0
+    for c, cs, tr, lens, acts, steps in ref_pin.micro_cases(n, "all"):
+        out, terminal = oc.replay_steps(tr, lens, steps, num_procs=n, cache_size=cs)
+        assert terminal and out.digest == int(c["digest"], 16), c["seed"]
+        k += 1
+    assert k == 160
+

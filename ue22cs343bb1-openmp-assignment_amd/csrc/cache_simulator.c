@@ -19,6 +19,10 @@
  *       later rounds are lockstep. FILE is plain rows, or a JSON record of tests/golden/schedules
  *       record (its "rounds" strings): e.g. tests/golden/schedules/test_4_run_3.json makes
  *       `cache_simulator test_4` write the accepted run_3
+ *   --micro FILE      a micro-step schedule (dash_set_micro_schedule): whitespace-separated
+ *       tokens, one per round, "P<t>" / "I<t>" / "S<t>" = node t steps (pops or issues, its
+ *       sends held), "D<t>" = node t delivers its oldest held message; plain text, or the
+ *       "steps" string of a JSON record (tests/golden/ref_runs/micro4.json's cases)
  *
  * Bulk modes (one GPU batch, many systems; dumps go to OUT_DIR/<k>/):
  *   --batch LIST        system k = the k-th trace directory listed in LIST (one per line)
@@ -40,6 +44,8 @@ static const char *txn_names[DASH_NUM_TXN] = {
 
 /* --rounds FILE: rows of n characters ('-' or a position digit); from a JSON record, the quoted
    strings after its "rounds" key. Returns the row count, or -1 on a malformed file. */
+static long read_micro(const char *path, unsigned n, uint8_t **out);
+
 static long read_rounds(const char *path, unsigned n, uint8_t **out) {
     FILE *f = fopen(path, "r");
     if (!f) return -1;
@@ -84,10 +90,50 @@ static long read_rounds(const char *path, unsigned n, uint8_t **out) {
     return rows;
 }
 
-/* dash_simulate_dir plus a schedule (seed or explicit rounds) and the event log of the one system */
+/* --micro FILE: one token per round, [PIS]<t> (a step) or D<t> (a delivery); from a JSON record, the
+   string after its "steps" key. Returns the round count, or -1 on a malformed file. */
+static long read_micro(const char *path, unsigned n, uint8_t **out) {
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    static char text[1 << 22];
+    size_t len = fread(text, 1, sizeof text - 1, f);
+    fclose(f);
+    text[len] = 0;
+    char *p = strstr(text, "\"steps\"");
+    if (p) {
+        p = strchr(p + 7, '"');
+        if (!p) return -1;
+        char *end = strchr(++p, '"');
+        if (!end) return -1;
+        *end = 0;
+    } else {
+        p = text;
+    }
+    long rows = 0, cap = 0;
+    uint8_t *r = NULL;
+    for (char *tok = strtok(p, " \t\r\n"); tok; tok = strtok(NULL, " \t\r\n")) {
+        char *e;
+        const long t = strtol(tok + 1, &e, 10);
+        if (!strchr("PISD", tok[0]) || e == tok + 1 || *e || t < 0 || t >= (long)n) { free(r); return -1; }
+        if (rows == cap) {
+            cap = cap ? 2 * cap : 256;
+            uint8_t *r2 = (uint8_t *)realloc(r, (size_t)cap * n);
+            if (!r2) { free(r); return -1; }
+            r = r2;
+        }
+        memset(r + rows * n, DASH_SIT_OUT, n);
+        r[rows * n + t] = tok[0] == 'D' ? DASH_MICRO_SEND : DASH_MICRO_STEP;
+        rows++;
+    }
+    *out = r;
+    return rows;
+}
+
+/* dash_simulate_dir plus a schedule (seed, explicit rounds or micro-steps) and the event log of the
+   one system */
 static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m, const char *out, int dev,
                            int dbg_instr, int dbg_msg, unsigned long long sched, const uint8_t *rounds,
-                           long nrounds, dash_stats *st) {
+                           long nrounds, int micro, dash_stats *st) {
     dash_cfg cfg = {0};
     cfg.num_procs = n;
     cfg.cache_size = cs;
@@ -104,7 +150,8 @@ static int simulate_traced(const char *dir, unsigned n, unsigned cs, unsigned m,
     dash_t *h = NULL;
     int rc = dash_create(&cfg, &h);
     if (rc != DASH_OK) return rc;
-    if (rounds) rc = dash_set_schedule(h, rounds, (uint32_t)nrounds);
+    if (rounds) rc = micro ? dash_set_micro_schedule(h, rounds, (uint32_t)nrounds)
+                           : dash_set_schedule(h, rounds, (uint32_t)nrounds);
     if (rc == DASH_OK && (rc = dash_load_dir(h, dir, 0)) == DASH_OK && (rc = dash_run(h, st)) == DASH_OK) {
         dash_node_state nodes[DASH_MAX_PROCS];
         rc = dash_read_state(h, 0, nodes);
@@ -237,7 +284,8 @@ static int run_synthetic(uint64_t count, const bulk_opts *o) {
 int main(int argc, char *argv[]) {
     unsigned n = 4, cs = 4, m = 32;
     int dev = 0, show = 0, dbg_instr = 0, dbg_msg = 0, n_given = 0;
-    const char *out = ".", *dir = NULL, *batch = NULL, *digests = NULL, *dump = NULL, *rounds_file = NULL;
+    const char *out = ".", *dir = NULL, *batch = NULL, *digests = NULL, *dump = NULL, *rounds_file = NULL,
+               *micro_file = NULL;
     unsigned long long synth = 0, seed = 0x5EED, sched = 0;
     unsigned len = 4096, kind = DASH_GEN_UNIFORM;
     double loc = 0.5;
@@ -258,6 +306,7 @@ int main(int argc, char *argv[]) {
         else if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = strtoull(argv[++i], NULL, 0);
         else if (!strcmp(argv[i], "--schedule") && i + 1 < argc) sched = strtoull(argv[++i], NULL, 0);
         else if (!strcmp(argv[i], "--rounds") && i + 1 < argc) rounds_file = argv[++i];
+        else if (!strcmp(argv[i], "--micro") && i + 1 < argc) micro_file = argv[++i];
         else if (!strcmp(argv[i], "--locality") && i + 1 < argc) loc = atof(argv[++i]);
         else if (!strcmp(argv[i], "--kind") && i + 1 < argc) {
             const char *k = argv[++i];
@@ -283,9 +332,14 @@ int main(int argc, char *argv[]) {
         fprintf(stderr, "cache_simulator: %s: not a round schedule for %u nodes\n", rounds_file, n);
         return EXIT_FAILURE;
     }
+    if (micro_file && !rounds_file && (nrounds = read_micro(micro_file, n, &rounds)) < 0) {
+        fprintf(stderr, "cache_simulator: %s: not a micro-step schedule for %u nodes\n", micro_file, n);
+        return EXIT_FAILURE;
+    }
     dash_stats st;
-    int rc = (dbg_instr || dbg_msg || sched || rounds_file)
-                 ? simulate_traced(dir, n, cs, m, out, dev, dbg_instr, dbg_msg, sched, rounds, nrounds, &st)
+    int rc = (dbg_instr || dbg_msg || sched || rounds)
+                 ? simulate_traced(dir, n, cs, m, out, dev, dbg_instr, dbg_msg, sched, rounds, nrounds,
+                                   micro_file && !rounds_file, &st)
                  : dash_simulate_dir(dir, n, cs, m, out, dev, &st);
     free(rounds);
     if (rc != DASH_OK) {

@@ -594,6 +594,17 @@ def test_engine_reenacts_non_round_model_runs(dash, n):
     assert reenact_micro(dash, n, "micro") == 40
 
 
+@pytest.mark.parametrize("N,CS", [(2, 1), (3, 3), (4, 4), (5, 16), (8, 2), (8, 4)])
+def test_micro_schedule_random_interleavings(dash, N, CS):
+    """MODE 4 beyond the reference's runs: random legal interleavings of the oracle's STRICT
+    micro-step model (tests/micro_fuzz.py: random traces, random node weights, run to
+    quiescence) drive the engine through dash_set_micro_schedule; every system ends in the
+    walk's final state with the walk's per-node sequence of pops and issues."""
+    import micro_fuzz
+    rng = np.random.default_rng(1000 + 10 * N + CS)
+    assert micro_fuzz.one_config(dash, rng, N, CS, 16, 40, random_batch) == []
+
+
 def test_set_micro_schedule_checks_its_input(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, schedule_seed=1) as eng:

@@ -602,7 +602,8 @@ def test_micro_schedule_random_interleavings(dash, N, CS):
     walk's final state with the walk's per-node sequence of pops and issues."""
     import micro_fuzz
     rng = np.random.default_rng(1000 + 10 * N + CS)
-    assert micro_fuzz.one_config(dash, rng, N, CS, 16, 40, random_batch) == []
+    bad, skipped = micro_fuzz.one_config(dash, rng, N, CS, 16, 40, random_batch)
+    assert bad == [] and len(skipped) < 4
 
 
 def test_set_micro_schedule_checks_its_input(dash):

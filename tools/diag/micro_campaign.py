@@ -25,18 +25,20 @@ def main():
     out = sys.argv[4] if len(sys.argv) > 4 else None
     dash = bench.load_dash()
     rng = np.random.default_rng(0x3C3C)
-    rep = {"configs": [], "systems": 0, "mismatched_systems": 0}
+    rep = {"configs": [], "systems": 0, "mismatched_systems": 0, "skipped_model_overflow": 0}
     t0 = time.time()
     for c in range(ncfg):
         N = int(rng.integers(1, 9))
         CS = int(rng.choice([1, 2, 3, 4, 5, 8, 16]))
         L = int(rng.integers(1, maxlen + 1))
-        bad = micro_fuzz.one_config(dash, rng, N, CS, nsys, L, random_batch)
+        bad, skipped = micro_fuzz.one_config(dash, rng, N, CS, nsys, L, random_batch)
         rep["configs"].append({"num_procs": N, "cache_size": CS, "max_len": L, "systems": nsys,
-                               "mismatched": bad[:8], "n_mismatched": len(bad)})
-        rep["systems"] += nsys
+                               "mismatched": bad[:8], "n_mismatched": len(bad), "skipped": skipped})
+        rep["systems"] += nsys - len(skipped)
         rep["mismatched_systems"] += len(bad)
-        print(f"[{time.time() - t0:.0f}s] cfg {c}: N={N} CS={CS} L={L} mismatched={len(bad)}", flush=True)
+        rep["skipped_model_overflow"] += len(skipped)
+        print(f"[{time.time() - t0:.0f}s] cfg {c}: N={N} CS={CS} L={L} mismatched={len(bad)} skipped={len(skipped)}",
+              flush=True)
     rep["seconds"] = time.time() - t0
     print(json.dumps({k: v for k, v in rep.items() if k != "configs"}), flush=True)
     if out:

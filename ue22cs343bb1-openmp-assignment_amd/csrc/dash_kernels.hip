@@ -678,7 +678,7 @@ void sim_kernel(const SimArgs a) {
     auto cap_check = [&](const uint32_t r0, mask_t& mMsg, mask_t& mIss) __attribute__((always_inline)) {
         if (M(r0 == cap) != 0) {  // wave-uniform: every system still active has run `cap` rounds
             COLD();
-            const bool kill = ((uint32_t)((mMsg | mIss) >> seg) & SEGMASK) != 0;
+            const bool kill = ((uint32_t)((mMsg | mIss | held()) >> seg) & SEGMASK) != 0;
             const mask_t mKill = M(kill);
             wmask &= ~mKill;
             mMsg &= ~mKill;
@@ -687,6 +687,7 @@ void sim_kernel(const SimArgs a) {
                 err |= DASH_ERR_ROUNDCAP_D;
                 cq = 0;
                 lenx = pc;
+                if constexpr (MICRO) on = 0;  // held sends die with the system (the loop must end)
             }
         }
     };

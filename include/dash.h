@@ -200,7 +200,8 @@ int dash_set_schedule(dash_t *h, const uint8_t *sched, uint32_t rounds);
    calls (:741-765) one by one while other threads run, so any interleaving of the reference's
    threads -- e.g. the one the oracle recovers from a reference run's DEBUG logs -- is one such
    schedule (tests/golden/ref_runs/). A valid schedule never steps a node whose outbox holds
-   messages. Runs at queue depth 256 only (no tiers); pass max_rounds >= the schedule's rounds. */
+   messages. Runs at queue depth 256 only (no tiers); pass max_rounds >= the schedule's rounds:
+   a system still active (or holding sends) at the round cap stops with DASH_ERR_ROUNDCAP. */
 #define DASH_MICRO_STEP 0u
 #define DASH_MICRO_SEND 1u
 int dash_set_micro_schedule(dash_t *h, const uint8_t *acts, uint32_t rounds);

@@ -51,7 +51,9 @@ static long read_rounds(const char *path, unsigned n, uint8_t **out) {
     if (!f) return -1;
     static char text[1 << 20];
     size_t len = fread(text, 1, sizeof text - 1, f);
+    const int more = fgetc(f) != EOF; /* a longer file would be cut: refuse it */
     fclose(f);
+    if (more) return -1;
     text[len] = 0;
     const char *p = strstr(text, "\"rounds\"");
     const int json = p != NULL;
@@ -97,7 +99,9 @@ static long read_micro(const char *path, unsigned n, uint8_t **out) {
     if (!f) return -1;
     static char text[1 << 22];
     size_t len = fread(text, 1, sizeof text - 1, f);
+    const int more = fgetc(f) != EOF;
     fclose(f);
+    if (more) return -1;
     text[len] = 0;
     char *p = strstr(text, "\"steps\"");
     if (p) {

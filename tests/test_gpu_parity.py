@@ -315,6 +315,28 @@ def test_debug_trace_other_shapes(dash, N, CS, seed):
             assert dash.format_events(eng.read_events(s)) == log, s
 
 
+def test_event_log_capacity_is_counted_in_rounds(dash):
+    """dash_cfg.trace_events counts rounds (include/dash.h): a log of exactly the run's rounds
+    holds every event; one whose capacity (rounded up to 4) ends before the last active round
+    reports DASH_ETRUNC."""
+    tr, lens = load_test_dir(GOLDEN / "test_4")
+    _, log = run_system(tr, lens, log=True, log_msgs=True)
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4096) as eng:
+        eng.load_traces(tr[None], lens[None])
+        rounds = eng.run()["rounds_max"]
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=rounds) as eng:
+        eng.load_traces(tr[None], lens[None])
+        eng.run()
+        assert dash.format_events(eng.read_events(0)) == log
+    short = (rounds - 1) // 4 * 4
+    assert 0 < short < rounds
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=short) as eng:
+        eng.load_traces(tr[None], lens[None])
+        eng.run()
+        with pytest.raises(dash.DashError):
+            eng.read_events(0)
+
+
 def test_debug_trace_truncation_is_reported(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4) as eng:

@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <memory>
 #include <vector>
 
 #include "dash.h"
@@ -741,18 +742,20 @@ static int write_digests_impl(dash_t* h, const char* path) {
     constexpr uint64_t CHUNK = 1u << 16;  // lines per chunk: <= 64 B each
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const uint64_t window = std::max<uint64_t>(1, std::min<uint64_t>(n, 2ull * nt * CHUNK));
-    std::vector<uint64_t> d(window);
-    std::vector<uint32_t> r(window), e(window);
+    // default-initialised (new T[]): zero-filling ~100 MB of buffers the writer overwrites anyway
+    // cost as much as the formatting (round 4: 26.5 ms per 1M systems)
+    std::unique_ptr<uint64_t[]> d(new uint64_t[window]);
+    std::unique_ptr<uint32_t[]> r(new uint32_t[window]), e(new uint32_t[window]);
     const uint64_t wch = (window + CHUNK - 1) / CHUNK;
-    std::vector<std::vector<char>> buf(wch);
-    for (auto& b : buf) b.resize(CHUNK * 64);
+    std::vector<std::unique_ptr<char[]>> buf(wch);
+    for (auto& b : buf) b.reset(new char[CHUNK * 64]);
     std::vector<size_t> used(wch);
     FILE* f = fopen(path, "w");
     if (!f) return fail(h, DASH_EIO, "open %s", path);
     bool ok = true;
     for (uint64_t w0 = 0; ok && w0 < n; w0 += window) {
         const uint64_t wn = std::min(window, n - w0);
-        int rc = dash_read_results(h, w0, wn, d.data(), r.data(), e.data());
+        int rc = dash_read_results(h, w0, wn, d.get(), r.get(), e.get());
         if (rc != DASH_OK) {
             fclose(f);
             return rc;
@@ -762,7 +765,7 @@ static int write_digests_impl(dash_t* h, const char* path) {
         auto work = [&] {  // touches only its chunks' preallocated buffers: nothing here allocates
             static const char HEX[] = "0123456789abcdef";
             for (uint64_t c; (c = next.fetch_add(1)) < nch;) {
-                char* o = buf[c].data();
+                char* o = buf[c].get();
                 auto dec = [&o](uint64_t v) {
                     char t[20];
                     int m = 0;
@@ -781,7 +784,7 @@ static int write_digests_impl(dash_t* h, const char* path) {
                     for (; sh >= 0; sh -= 4) *o++ = HEX[(e[k] >> sh) & 15];
                     *o++ = '\n';
                 }
-                used[c] = (size_t)(o - buf[c].data());
+                used[c] = (size_t)(o - buf[c].get());
             }
         };
         std::vector<std::thread> pool;
@@ -791,7 +794,7 @@ static int write_digests_impl(dash_t* h, const char* path) {
         }
         work();
         for (auto& th : pool) th.join();
-        for (uint64_t c = 0; ok && c < nch; c++) ok = fwrite(buf[c].data(), 1, used[c], f) == used[c];
+        for (uint64_t c = 0; ok && c < nch; c++) ok = fwrite(buf[c].get(), 1, used[c], f) == used[c];
     }
     return (fclose(f) == 0 && ok) ? DASH_OK : fail(h, DASH_EIO, "write %s", path);
 }

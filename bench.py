@@ -20,7 +20,12 @@ The headline line also carries `contention` (BASELINE configs[3], its own timed 
 one instance per host core = BASELINE.md mode (A)) and `cpu_port` (the oracle restatement
 on the same host).
 
-Prints ONE JSON line on rank 0 (contract in the task statement).
+Prints ONE JSON line on rank 0 (contract in the task statement), at most LINE_BUDGET (4 KB)
+long: the driver keeps only a ~10 KB tail of stdout + stderr, and round 4's 52-KB line was
+unreadable to it. The full record (per-point histograms, kernel times, CPU-baseline
+samples, box sysfs, next rows) goes to the side file named by the line's `detail` (--detail);
+the line itself is `compact_headline()` of that record. Stderr stays quiet: one progress line
+per sweep CACHE_SIZE.
 
 Other modes (not the headline): --kind contention (configs[3]); --sweep (configs[4]);
 --host-traces [--host-batches B] [--host-native]: traces handed over from host memory every
@@ -32,12 +37,15 @@ the CPU baseline instead of the reference binary.
 """
 import argparse
 import json
+import math
 import os
 import pathlib
 import sys
 import time
 
 ROOT = pathlib.Path(__file__).resolve().parent
+DETAIL_DEFAULT = ROOT / "gpurun_out" / "bench_detail.json"
+LINE_BUDGET = 4096  # bytes of the printed line
 PEAK_HBM = 8.0e12  # B/s, MI355X_MICROARCH.md chip table
 BYTES_PER_INSTR = 2  # packed trace record read once
 # VALU issue ceiling for this kernel's instruction forms (v_cndmask_e64, v_cmp_e64, v_bfe,
@@ -113,14 +121,15 @@ def ref_exe(cache_size):
     return ROOT / "oracle" / "_ref" / name
 
 
-def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, locality=0, kind_name=None):
+def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, locality=0, kind_name=None,
+                 min_batches=1):
     """The reference itself (oracle/_ref/cache_simulator_bench[_cs<C>]: assignment.c with the
     benchmark patch of SURVEY.md §8(d), gcc -O2 -fopenmp, 8 spinning OpenMP threads per
     instance) on systems 0.. of the same synthetic workload, written as the reference's
     tests/<dir>/core_<n>.txt. `instances` processes run concurrently (0 = one per host core,
     BASELINE.md mode (A): the north star's "as many concurrent instances as host cores";
-    1 = mode (B), one 8-thread instance); batches repeat until `target_s` has passed (at
-    least one batch)."""
+    1 = mode (B), one 8-thread instance); batches repeat until `target_s` has passed and at
+    least `min_batches` ran."""
     import subprocess
     import tempfile
     sys.path.insert(0, str(ROOT / "tests"))
@@ -185,7 +194,7 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
             instr += len(fin) * 8 * args.len
             elapsed += max(fin.values())
             rates.append(len(fin) * 8 * args.len / max(fin.values()))
-            if time.perf_counter() - t0 >= target_s:
+            if batches >= min_batches and time.perf_counter() - t0 >= target_s:
                 break
     cores = host_cores()
     loc = f", locality {locality / 65536:g}" if kind_name == "locality" else ""
@@ -347,22 +356,27 @@ def digest_sum(digests):
     return [int((d & np.uint64(0xFFFFFFFF)).sum(dtype=np.uint64)), int((d >> np.uint64(32)).sum(dtype=np.uint64))]
 
 
-def kernel_fingerprint(lib_path):
-    """sha256 prefix of the headline kernel's code + descriptor in the library being run
-    (tools/kernel_fingerprint.py), or None if it cannot be read."""
+def sim_symbol(cache_size):
+    """Mangled name of the first-tier lockstep kernel sim_kernel<8, CS, 16, 0> (8-node systems)."""
+    return f"_ZN4dash10sim_kernelILi8ELi{cache_size}ELj16ELi0EEEvNS_7SimArgsE"
+
+
+def kernel_fingerprint(lib_path, sym=None):
+    """sha256 prefix of a kernel's code + descriptor in the library being run (default the
+    headline sim_kernel<8,4,16,0>; tools/kernel_fingerprint.py), or None if it cannot be read."""
     sys.path.insert(0, str(ROOT / "tools"))
     try:
         import kernel_fingerprint as kf
-        return kf.fingerprint(lib_path)
+        return kf.fingerprint(lib_path, sym or kf.HEADLINE_SYM)
     except Exception:
         return None
 
 
-def read_profile(kind, fp):
+def read_profile(kind, fp, sym=None):
     """Per-launch counters of the first-tier sim_kernel from the committed rocprofv3
     PMC summary for this workload (tools/pmc_summary.py), only if it was measured on the
     code object being run: (profile or None, note). `fp` = kernel_fingerprint of the
-    library this process loaded."""
+    kernel (`sym`, default the headline's) in the library this process loaded."""
     f = ROOT / "profiles" / f"pmc_{kind}.json"
     if not f.exists():
         return None, f"{f.relative_to(ROOT)} missing"
@@ -372,8 +386,8 @@ def read_profile(kind, fp):
         return None, f"{f.relative_to(ROOT)} unreadable: {e}"
     if fp is None or prof.get("kernel_fingerprint") != fp:
         return None, (f"{f.relative_to(ROOT)} was measured on kernel {prof.get('kernel_fingerprint')}, this run's "
-                      f"sim_kernel<8,4,16,0> is {fp}: its counters do not describe this binary, so traffic "
-                      f"and issue figures are omitted")
+                      f"{sym or 'sim_kernel<8,4,16,0>'} is {fp}: its counters do not describe this binary, so "
+                      f"traffic and issue figures are omitted")
     return prof, None
 
 
@@ -391,8 +405,11 @@ def sweep_gpu(args, dash, rank, world, dev, steps, warmup):
     points = []
     a = argparse.Namespace(**vars(args))
     a.steps, a.warmup = steps, warmup
+    full = M == 1 << 20 and args.len == 4096  # per GPU: the size the committed PMC passes ran
     for cs in (1, 2, 4, 8, 16):
         eng = dash.Engine(M, num_procs=8, cache_size=cs, max_instr=args.len, device=dev)
+        t_cs = time.perf_counter()
+        fp = kernel_fingerprint(dash.LIB_PATH, sim_symbol(cs)) if full else None
         try:
             for c2, p in SWEEP_GRID:
                 if c2 != cs:
@@ -405,44 +422,56 @@ def sweep_gpu(args, dash, rank, world, dev, steps, warmup):
                     elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
                                               stats["dropped"]] + dsum, torch.device("cuda", dev), world)
                 avg_s = sum(kms) / len(kms) / 1e3
-                if rank == 0:  # progress (a long silent run looks hung)
-                    print(f"[sweep] CS {cs} locality {p}: {elapsed / steps * 1e3:.1f} ms/step", file=sys.stderr,
-                          flush=True)
+                # committed PMC passes of this point (tools/evidence_sweep_pmc.sh), only for the full-size
+                # workload and only when measured on this code object
+                prof, note = read_profile(f"sweep_cs{cs}_p{p:g}", fp, sim_symbol(cs)) if full else \
+                    (None, "committed PMC runs are of the full-size workload")
                 points.append({"cache_size": cs, "locality": p,
                                "value": world * M * 8 * args.len * steps / elapsed,
                                "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
                                # this rank's launches over the timed steps (HIP events; the step time above
                                # is the max over ranks of the whole timed region)
                                "kernel_ms_avg": avg_s * 1e3, "kernel_ms_steps": [round(x, 3) for x in kms],
-                               "roofline": roofline(M, args.len, avg_s, None,
-                                                    "no committed PMC run for sweep points: traffic not measured"),
+                               "roofline": roofline(M, args.len, avg_s, prof, note),
+                               "valu_issue": valu_issue(prof, stats["wave_rounds"]) if prof else None,
                                "rounds_per_system": totals[14] / (world * M),
+                               "wave_rounds": stats["wave_rounds"],
                                "hist": totals[:13], "instructions": totals[13], "rounds_total": totals[14],
                                "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19],
+                               # systems that hit the reference's undefined behaviour (DASH_ERR_OOB / CTZ0):
+                               # parity there is with the engine's defined drop rule
+                               "ub_frac": totals[15] / (world * M),
                                "tier_systems": stats["tier_systems"]})
         finally:
             eng.close()
+        if rank == 0:  # one progress line per CACHE_SIZE (stderr stays well under 1 KB)
+            print(f"[sweep] CS {cs}: 5 points in {time.perf_counter() - t_cs:.1f} s", file=sys.stderr, flush=True)
     return points
 
 
-def sweep_cpu(args, dash, points, target_s):
-    """The reference itself per sweep point (mode (A): one instance per host core, built for that
-    CACHE_SIZE, on systems 0.. of that point's locality traces): at least one batch, then more
-    until `target_s` has passed. Rank 0, after every GPU point and after the process group is
-    gone."""
-    for pt in points:
-        pt["cpu_baseline"], pt["vs_baseline"], pt["cpu_baseline_note"] = None, None, None
+def sweep_cpu(args, dash, points, target_s, min_batches=3):
+    """The reference itself per CACHE_SIZE: mode (A), one instance per host
+    core, the binary built for that CACHE_SIZE, on systems 0.. of the locality-0.5 traces, at least
+    `min_batches` batches (and `target_s` seconds); the figure (with its batch spread and stalled
+    instances) is the `cpu_baseline` of that CACHE_SIZE's five points. Rank 0, after every GPU
+    point and after the process group is gone. Returns {cs: baseline or None}."""
+    per_cs = {}
+    for cs in sorted({pt["cache_size"] for pt in points}):
+        per_cs[cs] = None
         if args.no_cpu_baseline:
             continue
-        print(f"[sweep] reference baseline CS {pt['cache_size']} locality {pt['locality']}", file=sys.stderr,
-              flush=True)
         try:
-            cpu = ref_baseline(args, args.seed, dash.GEN_LOCALITY, target_s, args.ref_instances,
-                               cache_size=pt["cache_size"], locality=int(round(pt["locality"] * 65536)),
-                               kind_name="locality")
-            pt["cpu_baseline"], pt["vs_baseline"] = cpu, pt["value"] / cpu["value"]
+            per_cs[cs] = ref_baseline(args, args.seed, dash.GEN_LOCALITY, target_s, args.ref_instances,
+                                      cache_size=cs, locality=32768, kind_name="locality", min_batches=min_batches)
         except Exception as e:  # reported, never substituted by the port
-            pt["cpu_baseline_note"] = f"reference baseline unavailable: {e}"
+            per_cs[cs] = {"error": f"reference baseline unavailable: {e}"}
+    for pt in points:
+        cpu = per_cs.get(pt["cache_size"])
+        ok = cpu is not None and "value" in cpu
+        pt["cpu_baseline"] = cpu if ok else None
+        pt["vs_baseline"] = pt["value"] / cpu["value"] if ok else None
+        pt["cpu_baseline_note"] = None if ok else (cpu or {}).get("error", "no CPU baseline (--no-cpu-baseline)")
+    return per_cs
 
 
 def sweep(args, dash, rank, world, dev):
@@ -453,17 +482,25 @@ def sweep(args, dash, rank, world, dev):
     if dist.is_initialized():
         dist.destroy_process_group()
     if rank == 0:
-        sweep_cpu(args, dash, points, args.sweep_cpu_seconds)
-        print(json.dumps({"metric": "simulated instr/sec (whole node), 8-core DASH systems; sweep",
-                          "unit": "instr/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "higher_is_better": True, "scaling": "weak", "dtype": "u8",
-                          "data": "synthetic locality traces (on-device generator, seed keyed by global id)",
-                          "config": {"workload": f"{world * M} systems ({M}/GPU) x 8 nodes x {args.len} "
-                                                 f"instr, CACHE_SIZE x locality grid (BASELINE configs[4])",
-                                     "parallelism": f"systems sharded over {world} GPU(s)"},
-                          "vs_baseline_basis": "per point: value / cpu_baseline.value (the reference binary built "
-                                               "for that CACHE_SIZE, mode (A), on systems 0.. of that point's traces)",
-                          "sweep": points}), flush=True)
+        per_cs = sweep_cpu(args, dash, points, args.sweep_cpu_seconds, args.sweep_cpu_batches)
+        detail = {"metric": "simulated instr/sec (whole node), 8-core DASH systems; sweep",
+                  "unit": "instr/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                  "higher_is_better": True, "scaling": "weak", "dtype": "u8",
+                  "data": "synthetic locality traces (on-device generator, seed keyed by global id)",
+                  "config": {"workload": f"{world * M} systems ({M}/GPU) x 8 nodes x {args.len} "
+                                         f"instr, CACHE_SIZE x locality grid (BASELINE configs[4])",
+                             "parallelism": f"systems sharded over {world} GPU(s)"},
+                  "vs_baseline_basis": SWEEP_CPU_BASIS,
+                  "sweep": {"steps": args.steps, "warmup": args.warmup, "cpu_per_cache_size": per_cs,
+                            "golden": sweep_golden_check(points, world * M, args), "points": points}}
+
+        def compact(d, shown):
+            out = {k: d[k] for k in ("metric", "unit", "n_gpus", "steps", "warmup", "higher_is_better",
+                                     "scaling", "dtype", "data", "config")}
+            out["sweep"] = compact_sweep(d["sweep"])
+            out["detail"] = str(shown)
+            return out
+        emit(detail, args.detail, compact)
 
 
 def host_trace_batch(seed, M, L):
@@ -739,6 +776,152 @@ def totals_dict(totals):
             "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19]}
 
 
+def rank_spread(x, device):
+    """[min, max] of a per-rank figure over the ranks (one MIN and one MAX all-reduce; [x, x]
+    without a process group)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return [x, x]
+    lo = torch.tensor([x], dtype=torch.float64, device=device)
+    hi = lo.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return [float(lo.item()), float(hi.item())]
+
+
+SWEEP_CPU_BASIS = ("per CACHE_SIZE: the reference built for it, mode (A), >= 3 batches on systems 0.. of the "
+                   "locality-0.5 traces; that figure is the cpu_baseline of the CACHE_SIZE's five points")
+
+
+def sig(x, n=4):
+    """x rounded to n significant digits (ints, bools and None unchanged): keeps the line short."""
+    if x is None or isinstance(x, (bool, int)) or not isinstance(x, float) or x == 0 or not math.isfinite(x):
+        return x
+    return float(f"{x:.{n - 1}e}")
+
+
+def compact_cpu(c, sample=True):
+    """The line's form of a reference / port CPU baseline: figure, cores, mode, batch spread."""
+    if not c or "value" not in c:
+        return None
+    out = {"value": sig(c["value"]), "unit": c.get("unit", "instr/s"), "cores": c.get("cores"),
+           "kind": c.get("kind")}
+    if c.get("mode"):
+        out["mode"] = c["mode"]
+    b = c.get("batches")
+    if b:
+        out["batches"] = [b["n"], sig(b["min"], 3), sig(b["median"], 3), sig(b["max"], 3)]
+    if "hung_instances_killed" in c:
+        out["hung"] = c["hung_instances_killed"]
+    if sample:
+        out["cpu_model"] = (c.get("cpu_model") or "")[:48]
+        out["sample"] = ((f"{c['instances']} concurrent instances x 8 OpenMP threads, assignment.c + bench patch, "
+                          f"gcc -O2 -fopenmp" if c.get("kind") == "reference" else
+                          "oracle/dash_oracle.c restatement, OpenMP over systems") + "; full text in detail")
+    return out
+
+
+def compact_roofline(r):
+    return {k: sig(r.get(k)) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")} if r else None
+
+
+def compact_headline(d, detail_path):
+    """The printed line (<= LINE_BUDGET bytes) from the full record `d`: the contract fields, roofline,
+    CPU baselines, and configs[3] / configs[4] / §8(f) / box summaries; everything else stays in
+    the side file `detail_path`."""
+    line = {k: d.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    for k in ("value", "ms_per_step", "vs_baseline"):
+        line[k] = sig(line[k], 5)
+    line["config"] = {"workload": d["config"]["workload"], "parallelism": d["config"]["parallelism"]}
+    line["rccl_world"] = d.get("rccl_world")
+    line["backend"] = d.get("backend")
+    line["kernel_ms_avg"] = sig(d.get("kernel_ms_avg"), 5)
+    line["kernel_ms_rank"] = [sig(x, 5) for x in d.get("kernel_ms_rank") or []]
+    line["roofline"] = compact_roofline(d.get("roofline"))
+    vi = d.get("valu_issue")
+    if vi:
+        line["valu_issue_frac"] = sig(vi.get("frac"), 3)
+    line["ub_frac"] = sig(d.get("ub_frac"), 3)
+    line["cpu_baseline"] = compact_cpu(d.get("cpu_baseline"))
+    if d.get("cpu_baseline_note"):
+        line["cpu_baseline_note"] = d["cpu_baseline_note"][:160]
+    if d.get("cpu_baseline_mode_b"):
+        line["vs_baseline_mode_b"] = sig(d.get("vs_baseline_mode_b"))
+        line["cpu_baseline_mode_b"] = compact_cpu(d["cpu_baseline_mode_b"], sample=False)
+    if d.get("cpu_port"):
+        line["cpu_port"] = sig(d["cpu_port"]["value"])
+    c = d.get("contention")
+    if c:
+        t = c["totals"]
+        line["contention"] = {"value": sig(c["value"], 5), "ms_per_step": sig(c["ms_per_step"], 5),
+                              "frac": sig(c["roofline"]["frac"]), "traffic": sig(c["roofline"].get("traffic")),
+                              "err_systems": t["err_systems"], "digest_sum": t["digest_sum"]}
+    if d.get("sweep"):
+        line["sweep"] = compact_sweep(d["sweep"])
+    nx = d.get("next")
+    if nx:
+        ev, sd = nx.get("events") or {}, nx.get("seeded") or {}
+        line["next"] = {"events_x": sig(ev.get("slowdown"), 3), "seeded_x": sig(sd.get("slowdown"), 3),
+                        "parity": bool(ev.get("parity_same_digests_as_fast") and ev.get("parity_events_logged")
+                                       and sd.get("parity_all_issued") and sd.get("parity_reproducible"))}
+    b = d.get("box") or {}
+    pb, pa = b.get("probe_before") or {}, b.get("probe_after") or {}
+    if pb or pa:
+        line["box"] = {"pci": ((pb.get("sysfs") or {}).get("pci")),
+                       "probe_ms": [pb.get("probe_ms"), pa.get("probe_ms")],
+                       "sclk_mhz": [pb.get("sclk_mhz"), pa.get("sclk_mhz")]}
+    line["kernel_fingerprint"] = d.get("kernel_fingerprint")
+    line["detail"] = str(detail_path)
+    return line
+
+
+def compact_sweep(sw):
+    """configs[4] in the line: one row per point, the reference per CACHE_SIZE, the golden flags."""
+    def giga(x):
+        return sig(x / 1e9, 4) if x is not None else None
+    rows = [[p["cache_size"], p["locality"], giga(p["value"]), sig(p["ms_per_step"]), sig(p["roofline"]["frac"], 3),
+             sig(p.get("vs_baseline"), 3), sig(p["ub_frac"], 3), giga(p["roofline"].get("traffic"))]
+            for p in sw["points"]]
+    cpu = {str(cs): ([c["batches"]["n"], sig(c["value"], 3), sig(c["batches"]["min"], 3),
+                      sig(c["batches"]["median"], 3), sig(c["batches"]["max"], 3), c["hung_instances_killed"]]
+                     if c and "value" in c else None)
+           for cs, c in (sw.get("cpu_per_cache_size") or {}).items()}
+    g = sw.get("golden")
+    return {"cols": ["cs", "p", "value_G", "ms_per_step", "frac", "vs_baseline", "ub_frac", "traffic_GB"],
+            "rows": rows, "steps": sw["steps"],
+            "cpu_cols": ["n", "value", "min", "median", "max", "hung"], "cpu": cpu,
+            "golden_bit_exact": ([x["bit_exact"] for x in g] if isinstance(g, list) else None)}
+
+
+def detail_path_arg(p):
+    """--detail PATH (relative paths are taken from the repo root, where the driver runs)."""
+    path = pathlib.Path(p) if p else DETAIL_DEFAULT
+    return path if path.is_absolute() else ROOT / path
+
+
+def emit(detail, detail_arg, compact=None):
+    """Write the full record to the side file and print the compact line (rank 0)."""
+    path = detail_path_arg(detail_arg)
+    shown = path.relative_to(ROOT) if path.is_relative_to(ROOT) else path
+    try:
+        path.parent.mkdir(parents=True, exist_ok=True)
+        path.write_text(json.dumps(detail, indent=1))
+    except OSError as e:
+        shown = f"unwritten ({e})"
+    line = (compact or compact_headline)(detail, shown)
+    text = json.dumps(line, separators=(",", ":"))
+    if len(text) > LINE_BUDGET:  # never silently: drop the least important summaries until it fits
+        for k in ("next", "box", "cpu_baseline_mode_b", "contention"):
+            line.pop(k, None)
+            line["dropped_for_size"] = line.get("dropped_for_size", []) + [k]
+            text = json.dumps(line, separators=(",", ":"))
+            if len(text) <= LINE_BUDGET:
+                break
+    print(text, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -758,8 +941,14 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target seconds of each CPU leg (reference mode A, mode B, oracle port)")
     ap.add_argument("--sweep-cpu-seconds", type=float, default=1.0,
-                    help="--sweep: target seconds of the reference baseline per point (at least one batch)")
+                    help="configs[4]: target seconds of the reference baseline per CACHE_SIZE (at least "
+                         "--sweep-cpu-batches batches)")
+    ap.add_argument("--sweep-cpu-batches", type=int, default=3,
+                    help="configs[4]: minimum reference batches per CACHE_SIZE")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--detail", default=None,
+                    help="side file for the full record (default gpurun_out/bench_detail.json; relative to the "
+                         "repo root); the printed line is its <= 4 KB summary and names it")
     ap.add_argument("--line-sweep", choices=["auto", "on", "off"], default="auto",
                     help="the configs[4] grid inside the headline line (`sweep` object): auto = only with the "
                          "full-size uniform headline workload")
@@ -830,9 +1019,15 @@ def main():
         owned[base:base + count] = 1
         if world > 1:
             dist.all_reduce(owned)
+        # the same fields the GPU line records: the group actually formed and a per-rank spread
+        # (here of rank + 1, so [1, world])
+        rccl_world = dist.get_world_size() if dist.is_initialized() else 1
+        backend = str(dist.get_backend()) if dist.is_initialized() else None
+        spread = rank_spread(float(rank + 1), torch.device("cpu"))
         if rank == 0:
             print(json.dumps({"world": world, "systems_owned": int(owned.sum()),
-                              "each_once": bool((owned == 1).all()), "local_rank": local_rank}), flush=True)
+                              "each_once": bool((owned == 1).all()), "local_rank": local_rank,
+                              "rccl_world": rccl_world, "backend": backend, "kernel_ms_rank": spread}), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -914,6 +1109,11 @@ def main():
         next_rows = {"events": bench_next.events_row(dash, dev, args.seed, args.next_event_systems, args.len),
                      "seeded": bench_next.seeded_row(dash, dev, args.seed, M, args.len, 1)}
 
+    # what the process group actually formed, and the spread of the headline
+    # kernel's average launch time over the ranks (one MIN and one MAX all-reduce)
+    rccl_world = dist.get_world_size() if dist.is_initialized() else 1
+    backend = str(dist.get_backend()) if dist.is_initialized() else None
+    k_rank = rank_spread(avg_kernel_s * 1e3, torch.device("cuda", dev))
     # the CPU legs run after the timed regions and after the process group is gone, on rank 0
     # only, for every --gpus N (the ratio north_star states is the 8-GPU one)
     if dist.is_initialized():
@@ -921,13 +1121,12 @@ def main():
     if rank == 0:
         sweep_obj = None
         if points is not None:
-            sweep_cpu(args, dash, points, 0.0)  # one batch of the reference per point
+            sweep_cpu_obj = sweep_cpu(args, dash, points, args.sweep_cpu_seconds, args.sweep_cpu_batches)
             sweep_obj = {"workload": f"{world * M} systems ({M}/GPU) x 8 nodes x {args.len} locality RD/WR per "
                                      f"node, CACHE_SIZE {{1,2,4,8,16}} x locality {{0,.25,.5,.75,1}} "
                                      f"(BASELINE configs[4]; seed 0x{args.seed:X}, keyed by global id)",
                          "steps": args.line_sweep_steps, "warmup": args.line_sweep_warmup,
-                         "cpu_baseline_basis": "per point: one batch of the reference built for that CACHE_SIZE, "
-                                               "mode (A), on systems 0.. of that point's traces",
+                         "cpu_baseline_basis": SWEEP_CPU_BASIS, "cpu_per_cache_size": sweep_cpu_obj,
                          "golden": sweep_golden_check(points, world * M, args), "points": points}
         cpu, cpu_b, port, note = None, None, None, None
         if not args.no_cpu_baseline:
@@ -945,7 +1144,7 @@ def main():
             port = cpu_baseline(args, args.seed, kind_id, locality, args.cpu_seconds)
             if args.cpu_kind == "port":
                 cpu, port = port, None
-        line = {
+        detail = {
             "metric": "simulated instr/sec (whole node), 8-core DASH systems; % HBM roofline",
             "value": value,
             "unit": "instr/s",
@@ -979,12 +1178,16 @@ def main():
             "cpu_baseline_note": note,
             "cpu_port": port,
             "kernel_ms_avg": avg_kernel_s * 1e3,
+            "kernel_ms_rank": k_rank,
             "kernel_ms_steps": [round(x, 3) for x in kernel_ms],
+            "rccl_world": rccl_world,
+            "backend": backend,
             "tier_systems": stats["tier_systems"],
             "wave_rounds": stats["wave_rounds"],
             # systems whose run hit the reference's undefined send to node 15 (ref :772,786):
             # parity there is with the engine's defined drop-and-flag rule
             "totals": totals_dict(totals),
+            "ub_frac": totals[15] / (world * M),
             "parity_note": ("totals.err_systems systems hit the reference's undefined behaviour (mostly the "
                             "send to node 15, assignment.c:772,786: DASH_ERR_OOB); on them parity is with the "
                             "engine's defined drop-and-flag rule (DESIGN.md §2), the rest with the reference's "
@@ -995,7 +1198,7 @@ def main():
             "box": dict(box_record(probe0, probe1),
                         sclk_during_timed_steps=sampler.summary() if sampler else None),
         }
-        print(json.dumps(line), flush=True)
+        emit(detail, args.detail)
 
 
 if __name__ == "__main__":

@@ -75,10 +75,14 @@ def test_bench_launches_its_own_ranks():
     lines come from this same command form); each global system lands on exactly one rank."""
     r, d = _bench("--gpus", "2", "--dist-selftest", "--systems", "1000")
     assert r.returncode == 0, r.stderr[-2000:]
-    assert d == {"world": 2, "systems_owned": 2000, "each_once": True, "local_rank": 0}
+    # the group the ranks actually formed, and the per-rank spread (MIN / MAX all-reduce of rank + 1)
+    assert d == {"world": 2, "systems_owned": 2000, "each_once": True, "local_rank": 0,
+                 "rccl_world": 2, "backend": "gloo", "kernel_ms_rank": [1.0, 2.0]}
     r, d = _bench("--gpus", "4", "--dist-selftest", "--systems", "5")
     assert r.returncode == 0, r.stderr[-2000:]
     assert d["world"] == 4 and d["systems_owned"] == 20 and d["each_once"]
+    assert d["rccl_world"] == 4 and d["kernel_ms_rank"] == [1.0, 4.0]
+    assert len(r.stdout.encode()) <= 4096 and len(r.stderr.encode()) <= 1024, (len(r.stdout), r.stderr)
 
 
 def test_bench_rejects_world_size_mismatch():

@@ -27,7 +27,13 @@ def _free_port():
 
 
 def _line(out):
-    return json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+    """The full record of a bench run: the side file its printed line names (read right after the
+    run, before another run overwrites it), with the printed line itself under "_line"."""
+    line = json.loads([x for x in out.splitlines() if x.startswith("{")][-1])
+    assert len(json.dumps(line, separators=(",", ":"))) <= 4096
+    d = json.loads((ROOT / line["detail"]).read_text())
+    d["_line"] = line
+    return d
 
 
 def test_two_ranks_match_one_process():
@@ -43,6 +49,10 @@ def test_two_ranks_match_one_process():
     assert one.returncode == 0, one.stderr[-3000:]
     d1 = _line(one.stdout)
     assert d2["n_gpus"] == 2 and d2["scaling"] == "weak"
+    # the group torchrun's ranks actually formed, per-rank kernel spread
+    assert d2["_line"]["rccl_world"] == 2 and d2["_line"]["backend"] == "gloo"
+    lo, hi = d2["_line"]["kernel_ms_rank"]
+    assert 0 < lo <= hi
     assert d2["totals"]["instructions_per_step"] == d1["totals"]["instructions_per_step"] == 4096 * 8 * 512
     assert d2["totals"]["hist"] == d1["totals"]["hist"]
     assert d2["totals"]["rounds_total"] == d1["totals"]["rounds_total"]
@@ -65,6 +75,7 @@ def test_bench_spawns_two_ranks_without_torchrun():
     assert one.returncode == 0, one.stderr[-3000:]
     d1 = _line(one.stdout)
     assert d2["n_gpus"] == 2 and d1["n_gpus"] == 1
+    assert d2["rccl_world"] == 2 and d1["rccl_world"] == 1 and d1["backend"] is None
     assert d2["totals"] == d1["totals"]
     assert d2["contention"]["totals"] == d1["contention"]["totals"]
     assert d2["contention"]["totals"]["instructions_per_step"] == 4096 * 8 * 512
@@ -105,7 +116,7 @@ def test_rccl_collectives_one_rank():
                          capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert one.returncode == 0, one.stderr[-3000:]
     d1 = _line(one.stdout)
-    assert dp["n_gpus"] == 1
+    assert dp["n_gpus"] == 1 and dp["rccl_world"] == 1 and dp["backend"] == "nccl"
     assert dp["totals"] == d1["totals"] and dp["contention"]["totals"] == d1["contention"]["totals"]
 
 

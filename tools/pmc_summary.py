@@ -8,9 +8,10 @@ counters were collected (tcc1 pass) the read bytes are the size-weighted sum
 RDREQ_128B x 128 + RDREQ_64B x 64 + RDREQ_32B x 32 (disjoint on this part: the
 uniform launch measured RDREQ 3.038e9 = 128B 3.038e9 + 64B 2.5e4 + 32B 0);
 otherwise 2 x FETCH_SIZE. WRITE_SIZE is taken as measured (KiB).
-The summary records the fingerprint of the headline kernel in the library the passes ran
-(tools/kernel_fingerprint.py; $DASH_LIB or the in-tree libdash.so): bench.py uses the file only
-for that code object.
+The summary records the fingerprint of the measured kernel in the library the passes ran
+(tools/kernel_fingerprint.py; $DASH_LIB or the in-tree libdash.so; $DASH_KSYM names the kernel's
+symbol, default the headline sim_kernel<8,4,16,0>): bench.py uses the file only for that code
+object. The wave-rounds of the launch (the engine's statistic) come from the pass's bench line.
 Usage: python tools/pmc_summary.py KIND KERNEL_SUBSTRING OUT_JSON DIR [DIR ...]"""
 import collections
 import csv
@@ -42,7 +43,8 @@ for d in sys.argv[4:]:
         agg[row["Counter_Name"]] += float(row["Counter_Value"])
         dur[row["Counter_Name"]] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
 res = {"kernel": kname, "workload": kind, "source": " ".join(sys.argv[4:]),
-       "kernel_fingerprint": kernel_fingerprint.fingerprint(os.environ.get("DASH_LIB") or kernel_fingerprint.LIB)}
+       "kernel_fingerprint": kernel_fingerprint.fingerprint(os.environ.get("DASH_LIB") or kernel_fingerprint.LIB,
+                                                     os.environ.get("DASH_KSYM") or kernel_fingerprint.HEADLINE_SYM)}
 for k in sorted(agg):
     res[k.lower()] = agg[k]
 read = None
@@ -93,5 +95,34 @@ for d in sys.argv[4:]:
                   "probe_ms": [pb.get("probe_ms"), pa.get("probe_ms")], "kernel_ms_avg": line.get("kernel_ms_avg")})
 if boxes:
     res["boxes"] = boxes
+# per wave-round figures (the engine's wave_rounds statistic of the same launch, from a pass's line):
+# what the sweep's CACHE_SIZE points differ in
+wr, instr = None, None
+for d in sys.argv[4:]:
+    try:
+        line = json.loads([x for x in pathlib.Path(d.rstrip("/") + ".log").read_text().splitlines()
+                           if x.startswith("{")][-1])
+        wr = line.get("wave_rounds")
+        instr = (line.get("totals") or {}).get("instructions_per_step")
+    except (OSError, IndexError, ValueError):
+        continue
+    if wr:
+        break
+if wr:
+    res["wave_rounds"] = wr
+    for k, name in (("SQ_INSTS_VALU", "valu"), ("SQ_INSTS_SALU", "salu"), ("SQ_INSTS_LDS", "lds"),
+                    ("SQ_INSTS_BRANCH", "branch"), ("SQ_INSTS_SMEM", "smem"), ("SQ_INSTS_VMEM_RD", "vmem_rd")):
+        if k in agg:
+            res[f"{name}_per_wave_round"] = agg[k] / wr
+    if "kernel_ms" in res:
+        # CU-cycles at the 2.4-GHz clock limit per wave-round and CU (256 CUs)
+        res["ns_per_wave_round_per_cu"] = res["kernel_ms"] * 1e6 * 256 / wr
+if "SQ_LDS_BANK_CONFLICT" in agg and agg.get("SQ_LDS_IDX_ACTIVE"):
+    res["lds_bank_conflict_frac"] = agg["SQ_LDS_BANK_CONFLICT"] / agg["SQ_LDS_IDX_ACTIVE"]
+if "SQ_WAVE_CYCLES" in agg and agg.get("SQ_BUSY_CU_CYCLES"):
+    # mean resident waves per CU: wave-cycles over busy CU-cycles (both in quad-cycle units on gfx950)
+    res["waves_per_cu"] = agg["SQ_WAVE_CYCLES"] / agg["SQ_BUSY_CU_CYCLES"] * 4
+if "read_bytes_per_launch" in res and instr:
+    res["fill_bytes_per_algorithmic_byte"] = res["read_bytes_per_launch"] / (2 * instr)  # 2 B per instruction
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

@@ -62,6 +62,9 @@ extern "C" {
 #define DASH_ERR_STUCK 32u    /* a receiver queue reached MSG_BUFFER_SIZE (256): head == tail, so the
                                  reference never drains it again (:167-170); its messages stay
                                  unhandled and later sends to it drop (:754-761). Modelled exactly. */
+#define DASH_ERR_SCHEDULE 64u /* a micro-step schedule stepped a node whose outbox still held sends
+                                 (not a reference interleaving: sendMessage is synchronous,
+                                 :741-765); the system stops there and its results are void */
 
 /* transactionType ordinals (ref :30-44) */
 enum dash_txn {
@@ -90,9 +93,10 @@ typedef struct dash_cfg {
     int32_t device;       /* HIP device ordinal */
     uint32_t trace_events; /* event log capacity for DEBUG_MSG / DEBUG_INSTR emission
                               (ref :179-182, :649-652), in rounds: every node's events of the
-                              first trace_events rounds (a node logs at most one event per
-                              round, so also at most trace_events events per node); 0 = no
-                              log; < 2^30; device memory num_systems x num_procs x 4 B each */
+                              first trace_events rounds, rounded up to a multiple of 4 (a node
+                              logs at most one event per round, so also at most that many events
+                              per node); 0 = no log; < 2^30; device memory num_systems x
+                              num_procs x 4 B per kept round */
     uint64_t schedule_seed; /* 0: lowest-sender-first lockstep (the parity schedule); else a
                                seeded legal schedule: per round a node sits out w.p. 1/4 and
                                senders deliver in a seeded order */
@@ -200,7 +204,8 @@ int dash_set_schedule(dash_t *h, const uint8_t *sched, uint32_t rounds);
    calls (:741-765) one by one while other threads run, so any interleaving of the reference's
    threads -- e.g. the one the oracle recovers from a reference run's DEBUG logs -- is one such
    schedule (tests/golden/ref_runs/). A valid schedule never steps a node whose outbox holds
-   messages. Runs at queue depth 256 only (no tiers); pass max_rounds >= the schedule's rounds:
+   messages; a system whose schedule does stops at that round with DASH_ERR_SCHEDULE. Runs at
+   queue depth 256 only (no tiers); pass max_rounds >= the schedule's rounds:
    a system still active (or holding sends) at the round cap stops with DASH_ERR_ROUNDCAP. */
 #define DASH_MICRO_STEP 0u
 #define DASH_MICRO_SEND 1u
@@ -211,8 +216,9 @@ int dash_read_results(dash_t *h, uint64_t first, uint64_t count, uint64_t *diges
                       uint32_t *rounds, uint32_t *errors);
 int dash_read_hist(dash_t *h, uint64_t sys, uint32_t *hist /* [DASH_NUM_TXN] */);
 /* The event log of one system, merged in lockstep order (round, then node): up to
-   cap events into out, the total into *n. DASH_ETRUNC if events fell past the log's
-   trace_events rounds (counted in *n, not kept). */
+   cap events into out, the total into *n (cap 0 with out NULL: count only). The log keeps
+   trace_events rounds rounded up to a multiple of 4 (a node logs at most one event per round);
+   DASH_ETRUNC if events fell past them (counted in *n, not kept). */
 int dash_read_events(dash_t *h, uint64_t sys, dash_event *out, uint32_t cap, uint32_t *n);
 /* HIP stream the engine launches on (hipStream_t as void*) */
 void *dash_stream(dash_t *h);

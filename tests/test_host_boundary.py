@@ -139,3 +139,24 @@ def test_create_error_message_describes_this_call(dash, tmp_path):
     with pytest.raises(dash.DashError) as e:
         dash.Engine(4, num_procs=8, cache_size=17)
     assert "cache_size" in str(e.value)
+
+
+def test_cli_refuses_conflicting_or_empty_schedules(dash, tmp_path):
+    """`--rounds` with `--micro` is refused (one would be dropped silently), and so is
+    an empty micro-step schedule (it would fall through to a plain lockstep run). Both are
+    argument errors reported before the GPU is touched."""
+    import shutil
+    import subprocess
+    exe = dash.PKG / "cache_simulator"
+    (tmp_path / "tests").mkdir()
+    shutil.copytree(GOLDEN / "test_4", tmp_path / "tests" / "test_4")
+    (tmp_path / "empty.txt").write_text("\n")
+    (tmp_path / "one.txt").write_text("P0\n")
+    (tmp_path / "r.txt").write_text("0123\n")
+    p = subprocess.run([str(exe), "test_4", "--rounds", "r.txt", "--micro", "one.txt"], cwd=tmp_path,
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 1 and "exclusive" in p.stderr
+    p = subprocess.run([str(exe), "test_4", "--micro", "empty.txt"], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=60)
+    assert p.returncode == 1 and "empty micro-step schedule" in p.stderr
+    assert not (tmp_path / "core_0_output.txt").exists()

@@ -332,18 +332,25 @@ int main(int argc, char *argv[]) {
     }
     uint8_t *rounds = NULL;
     long nrounds = 0;
+    if (rounds_file && micro_file) {  /* two schedules for one run: refuse rather than drop one */
+        fprintf(stderr, "cache_simulator: --rounds and --micro are exclusive\n");
+        return EXIT_FAILURE;
+    }
     if (rounds_file && (nrounds = read_rounds(rounds_file, n, &rounds)) < 0) {
         fprintf(stderr, "cache_simulator: %s: not a round schedule for %u nodes\n", rounds_file, n);
         return EXIT_FAILURE;
     }
-    if (micro_file && !rounds_file && (nrounds = read_micro(micro_file, n, &rounds)) < 0) {
-        fprintf(stderr, "cache_simulator: %s: not a micro-step schedule for %u nodes\n", micro_file, n);
+    if (micro_file && (nrounds = read_micro(micro_file, n, &rounds)) <= 0) {
+        /* an empty micro-step schedule would fall through to a plain lockstep run */
+        fprintf(stderr, "cache_simulator: %s: %s\n", micro_file,
+                nrounds == 0 ? "empty micro-step schedule" : "not a micro-step schedule");
+        free(rounds);
         return EXIT_FAILURE;
     }
     dash_stats st;
     int rc = (dbg_instr || dbg_msg || sched || rounds)
                  ? simulate_traced(dir, n, cs, m, out, dev, dbg_instr, dbg_msg, sched, rounds, nrounds,
-                                   micro_file && !rounds_file, &st)
+                                   micro_file != NULL, &st)
                  : dash_simulate_dir(dir, n, cs, m, out, dev, &st);
     free(rounds);
     if (rc != DASH_OK) {

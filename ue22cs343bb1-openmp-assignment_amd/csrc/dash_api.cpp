@@ -622,18 +622,29 @@ int dash_read_events(dash_t* h, uint64_t sys, dash_event* out, uint32_t cap, uin
         if (!h->d_events) return fail(h, DASH_ESTATE, "created with trace_events = 0");
         if (sys >= h->cfg.num_systems) return fail(h, DASH_EINVAL, "system out of range");
         const uint32_t N = h->cfg.num_procs, R = h->ev_rounds;
-        std::vector<uint32_t> cnt(N), ev((size_t)N * R);
+        std::vector<uint32_t> cnt(N);
+        uint32_t sys_rounds = 0;
         HIPCHK(h, hipSetDevice(h->cfg.device));
         HIPCHK(h, hipMemcpyAsync(cnt.data(), h->d_event_count + sys * N, N * 4, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(h, hipMemcpyAsync(ev.data(), h->d_events + sys * N * (uint64_t)R, ev.size() * 4, hipMemcpyDeviceToHost,
-                                 h->stream));
+        HIPCHK(h, hipMemcpyAsync(&sys_rounds, h->d_rounds + sys, 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
+        // only this run's rounds: the kernel writes the log up to its wave's last trip and never
+        // clears it, so rows past the system's last active round may hold an earlier run's words
+        // (ADVICE r4). Events only happen in rounds < rounds[sys]; copy whole 4-round rows of those.
+        const uint32_t Rs = std::min<uint32_t>(R, (uint32_t)std::min<uint64_t>(((uint64_t)sys_rounds + 3u) & ~3ull,
+                                                                                 0xFFFFFFFCull));
+        std::vector<uint32_t> ev((size_t)N * Rs);
+        if (Rs) {
+            HIPCHK(h, hipMemcpyAsync(ev.data(), h->d_events + sys * N * (uint64_t)R, ev.size() * 4,
+                                     hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
         // the log is round-major (a node logs at most one event per round): reading it round by
         // round, node by node, is the lockstep order
         uint64_t total = 0, logged = 0;
         for (uint32_t t = 0; t < N; t++) total += cnt[t];
         uint32_t k = 0;
-        for (uint32_t r = 0; r < R; r++)
+        for (uint32_t r = 0; r < std::min(Rs, sys_rounds); r++)
             for (uint32_t t = 0; t < N; t++) {
                 const uint32_t w = ev[(size_t)(r / 4) * N * 4 + t * 4 + r % 4];
                 if (!(w & 0x01000000u)) continue;  // bit 24: an event

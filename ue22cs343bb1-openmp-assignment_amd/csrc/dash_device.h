@@ -12,6 +12,7 @@ constexpr uint32_t DASH_ERR_CTZ0_D = 4u;
 constexpr uint32_t DASH_ERR_DEADLOCK_D = 8u;
 constexpr uint32_t DASH_ERR_ROUNDCAP_D = 16u;
 constexpr uint32_t DASH_ERR_STUCK_D = 32u;
+constexpr uint32_t DASH_ERR_SCHEDULE_D = 64u;
 
 // device statistics block (u64 words)
 enum : uint32_t {

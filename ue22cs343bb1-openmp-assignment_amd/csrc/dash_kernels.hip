@@ -583,6 +583,10 @@ void sim_kernel(const SimArgs a) {
         mask_t xVP = mVP, xVB = mVB, xRID = mRID;
         uint32_t xdP = dP, xwP = wP;
         if constexpr (MICRO) {
+            // a node told to step while its outbox still holds sends is not a reference
+            // interleaving (sendMessage completes before the thread's next pop or issue) and
+            // would overrun the 8-entry outbox: flagged and stopped below
+            const mask_t mBad = M(wp == 1u && on != 0u);
             auto push = [&](uint32_t w, uint32_t d) {
                 const uint32_t e = L::WORDS + ((oh + on) & (OUTBOX - 1u)) * 128u + lane;
                 lds[e] = w;
@@ -595,6 +599,17 @@ void sim_kernel(const SimArgs a) {
             }
             if (B(mVP)) push(wP, dP);
             if (B(mVB)) push(wA, msr);
+            if (mBad != 0) {  // the pushes above stayed in this lane's own outbox column
+                COLD();
+                err |= B(mBad) ? DASH_ERR_SCHEDULE_D : 0u;
+                const bool kill = ((uint32_t)(mBad >> seg) & SEGMASK) != 0;
+                wmask &= ~M(kill);
+                if (kill) {  // the system stops: nothing held, nothing to pop or issue
+                    cq = 0;
+                    lenx = pc;
+                    on = 0;
+                }
+            }
             const bool snd = wp == 2u && on != 0u;
             xdP = lds[L::WORDS + oh * 128u + 64 + lane];
             xwP = lds[L::WORDS + oh * 128u + lane];

@@ -40,6 +40,7 @@ TXN_NAMES = ("READ_REQUEST", "WRITE_REQUEST", "REPLY_RD", "REPLY_WR", "REPLY_ID"
 OK, EINVAL, EIO, EPARSE, EADDR, EDEVICE, ENOMEM, ESTATE, ETRUNC = 0, -1, -2, -3, -4, -5, -6, -7, -8
 EV_MSG, EV_INSTR = 0, 1
 ERR_OVERFLOW, ERR_OOB, ERR_CTZ0, ERR_DEADLOCK, ERR_ROUNDCAP, ERR_STUCK = 1, 2, 4, 8, 16, 32
+ERR_SCHEDULE = 64  # a micro-step schedule stepped a node with held sends (dash.h)
 KEEP_STATE = 1
 TIER_FROM_32, TIER_FROM_256 = 2, 4
 TEST_SHORT_ARB = 8  # testing only (dash.h)
@@ -365,9 +366,12 @@ class Engine:
 
     def read_events(self, sys: int) -> list:
         """The system's DEBUG_MSG / DEBUG_INSTR events in lockstep order (needs trace_events)."""
-        cap = self.cfg.trace_events * self.num_procs
-        arr = (Event * max(cap, 1))()
         n = ctypes.c_uint32()
+        # count first (cap 0), then read exactly that many: the log keeps trace_events rounded up to
+        # a multiple of 4 rounds, so trace_events * num_procs can undercount it (ADVICE r4)
+        _check(lib().dash_read_events(self.h, sys, None, 0, ctypes.byref(n)), "dash_read_events", self.h)
+        cap = n.value
+        arr = (Event * max(cap, 1))()
         _check(lib().dash_read_events(self.h, sys, arr, cap, ctypes.byref(n)), "dash_read_events", self.h)
         return list(arr[:min(n.value, cap)])
 

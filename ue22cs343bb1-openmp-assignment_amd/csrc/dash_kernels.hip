@@ -50,9 +50,17 @@ enum : uint32_t { D_EM = 0, D_S = 1, D_U = 2 };              // directoryEntrySt
 constexpr uint32_t OUTBOX = 8;  // MODE 4: held sends per node (one step: at most 7 INVs + one notice)
 constexpr uint32_t WIN = 2;        // trace window chunks per lane (enough: see the refill)
 constexpr uint32_t CHUNK = CHUNK_INSTR;   // instructions per 8-B HBM trace chunk (layout unit)
-constexpr uint32_t WCHUNK = DASH_WCHUNK;  // instructions per window refill (2: 4-B, 4: 8-B loads)
-static_assert(WCHUNK == 2 || WCHUNK == 4, "window chunk");
-using wchunk_t = typename std::conditional<WCHUNK == 4, uint2, uint32_t>::type;
+#ifndef DASH_WCHUNK_CS8
+#define DASH_WCHUNK_CS8 2
+#endif
+// instructions per window refill (2: 4-B, 4: 8-B loads). CACHE_SIZE 8 refills 2 at a time: its
+// cache rows make 9,212 B of LDS with 4-instruction chunks, which admits 16 waves per CU (the
+// measured residency, profiles/pmc_sweep_cs8_p0.json); 2-instruction chunks take the window from
+// 1,024 to 512 B, so the kernel has CACHE_SIZE 4's 8,700 B and its 18 waves
+template <int CS>
+constexpr uint32_t wchunk_of() { return CS == 8 ? DASH_WCHUNK_CS8 : DASH_WCHUNK; }
+static_assert(DASH_WCHUNK == 2 || DASH_WCHUNK == 4, "window chunk");
+static_assert(DASH_WCHUNK_CS8 == 2 || DASH_WCHUNK_CS8 == 4, "window chunk");
 #ifndef DASH_QCHECK
 #define DASH_QCHECK 4              // rounds between quiescence votes: one trip of the round loop (WCHUNK or 2 x WCHUNK)
 #endif
@@ -120,7 +128,7 @@ struct Lds {  // 32-bit word offsets
     static constexpr uint32_t CAC = ENT + 16 * 64 / 2;      // u16 [CS][64]  addr | value<<8      (swizzled)
     static constexpr uint32_t RNG = CAC + cs_rows<CS>() * 64 / 2;  // u32 [RING][64] message words
     static constexpr uint32_t WND = RNG + RING * 64;        // u16 [WIN*WCHUNK][64] trace window (swizzled)
-    static constexpr uint32_t WORDS = WND + WIN * WCHUNK * 64 / 2;
+    static constexpr uint32_t WORDS = WND + WIN * wchunk_of<CS>() * 64 / 2;
 };
 
 __device__ __forceinline__ void chunk_words(uint2 v, uint32_t& x, uint32_t& y) { x = v.x; y = v.y; }
@@ -184,6 +192,8 @@ void sim_kernel(const SimArgs a) {
     constexpr bool ARB = MODE == 1 || MODE == 3 || MICRO;  // the seeded / explicit schedule is on
     constexpr bool EVLOG = MODE >= 2;              // the DEBUG event log is on
     using L = Lds<P, CS, RING>;
+    constexpr uint32_t WCHUNK = wchunk_of<CS>();
+    using wchunk_t = typename std::conditional<WCHUNK == 4, uint2, uint32_t>::type;
     const uint32_t ncs = CS ? (uint32_t)CS : a.cache_size;  // cache lines per node
     constexpr uint32_t SPW = 64 / P;
     constexpr uint32_t SEGMASK = (1u << P) - 1u;

@@ -14,7 +14,7 @@ for pt in $POINTS; do
     step "cs $cs p $p pass $name"
     timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$D/$name" -o run -- \
         python3 bench.py --kind locality --locality "$p" --cache-size "$cs" --steps 1 --warmup 0 \
-        --no-cpu-baseline --contention-steps 0 --line-sweep off --line-next off \
+        --no-cpu-baseline --contention-steps 0 --line-sweep off --line-next off --detail "$D/$name.detail.json" \
         > "$D/$name.log" 2>&1 || { echo "pass $name failed"; exit 1; }
   }
   pass sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY

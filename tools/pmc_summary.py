@@ -78,13 +78,29 @@ if "SQ_ACTIVE_INST_VALU2" in agg and "SQ_CYCLES" in agg and "SQ_INSTS_VALU" in a
     res["valu_dual_issue_frac"] = agg["SQ_ACTIVE_INST_VALU2"] / q
 if "SQ_THREAD_CYCLES_VALU" in agg and "SQ_INSTS_VALU" in agg:
     res["valu_exec_lanes"] = agg["SQ_THREAD_CYCLES_VALU"] / agg["SQ_INSTS_VALU"]  # of 64
+
+
+def pass_record(d):
+    """The bench record of a pass: its line (DIR.log), or -- since round 5, when the line is the
+    compact summary -- the full record in the pass's side file (DIR.detail.json, else the path
+    the line names)."""
+    log = pathlib.Path(d.rstrip("/") + ".log")
+    line = json.loads([x for x in log.read_text().splitlines() if x.startswith("{")][-1])
+    if "totals" in line:
+        return line
+    side = pathlib.Path(d.rstrip("/") + ".detail.json")
+    if not side.exists() and line.get("detail"):
+        side = pathlib.Path(line["detail"])
+        side = side if side.is_absolute() else pathlib.Path(__file__).resolve().parent.parent / side
+    return json.loads(side.read_text())
+
+
 # the box each pass ran on (bench.py's `box` object, round 4), from the pass's own line (DIR.log),
 # so a reader can compare the PMC box with the box of the bench line these counters annotate
 boxes = []
 for d in sys.argv[4:]:
-    log = pathlib.Path(d.rstrip("/") + ".log")
     try:
-        line = json.loads([x for x in log.read_text().splitlines() if x.startswith("{")][-1])
+        line = pass_record(d)
     except (OSError, IndexError, ValueError):
         continue
     b = line.get("box") or {}
@@ -100,8 +116,7 @@ if boxes:
 wr, instr = None, None
 for d in sys.argv[4:]:
     try:
-        line = json.loads([x for x in pathlib.Path(d.rstrip("/") + ".log").read_text().splitlines()
-                           if x.startswith("{")][-1])
+        line = pass_record(d)
         wr = line.get("wave_rounds")
         instr = (line.get("totals") or {}).get("instructions_per_step")
     except (OSError, IndexError, ValueError):

@@ -62,10 +62,12 @@ def _sweep_points(path):
     return sw["points"] if isinstance(sw, dict) else sw
 
 
-@pytest.mark.parametrize("path", ["profiles/r03/final/sweep.json", "profiles/r04/bench_headline.json"])
+@pytest.mark.parametrize("path", ["profiles/r03/final/sweep.json", "profiles/r04/bench_headline.json",
+                                  "profiles/r05/ev5_b/bench_detail.json"])
 def test_committed_sweep_points_match_oracle_full_size(path):
     """configs[4] at full size: three grid points of the committed GPU lines --
-    round 3's `bench.py --sweep` and round 4's default headline line, whose `sweep` object the
+    round 3's `bench.py --sweep`, round 4's default headline line and round 5's side file of the
+    driver's command (the line itself carries the compact rows), whose `sweep` object the
     driver now times -- equal the oracle's run over all 2^20 systems (tests/golden/sweep_full.json,
     make_sweep_full.py): histograms, instructions, rounds, error systems, digest checksum."""
     f = ROOT / path

@@ -690,6 +690,9 @@ def valu_issue(prof, wave_rounds):
             "lds_bank_conflict_frac": (prof["sq_lds_bank_conflict"] / prof["sq_lds_idx_active"]
                                        if prof.get("sq_lds_idx_active") else None),
             "l2_hit_rate": prof.get("l2_hit_rate"),
+            # mean resident waves per CU over the launch (SQ_WAVE_CYCLES / SQ_BUSY_CU_CYCLES x 4)
+            "waves_per_cu": (prof["sq_wave_cycles"] / prof["sq_busy_cu_cycles"] * 4
+                             if prof.get("sq_wave_cycles") and prof.get("sq_busy_cu_cycles") else None),
             "vector_pipe": vector_pipe(prof, wr),
             # measured (SQ_ACTIVE_INST_VALU2, SQ_CYCLES): SIMD quad-cycles that issued one or two
             # VALU / two VALU, and the mean active lanes of a VALU instruction
@@ -841,8 +844,11 @@ def compact_headline(d, detail_path):
     line["kernel_ms_rank"] = [sig(x, 5) for x in d.get("kernel_ms_rank") or []]
     line["roofline"] = compact_roofline(d.get("roofline"))
     vi = d.get("valu_issue")
-    if vi:
-        line["valu_issue_frac"] = sig(vi.get("frac"), 3)
+    if vi:  # VALU busy, LDS bank conflicts and occupancy beside the roofline
+        line["issue"] = {"valu_frac": sig(vi.get("frac"), 3),
+                         "valu_busy": sig((vi.get("issue_slots") or {}).get("busy_frac"), 3),
+                         "lds_conflict": sig(vi.get("lds_bank_conflict_frac"), 3),
+                         "waves_per_cu": sig(vi.get("waves_per_cu"), 3)}
     line["ub_frac"] = sig(d.get("ub_frac"), 3)
     line["cpu_baseline"] = compact_cpu(d.get("cpu_baseline"))
     if d.get("cpu_baseline_note"):

@@ -59,7 +59,9 @@ def synthetic_detail(world=8, with_all=True):
         "config": {"workload": f"{M} systems/GPU x 8 nodes x 4096 uniform RD/WR per node, CACHE_SIZE=4",
                    "systems_per_gpu": M, "num_procs": 8, "instr_per_node": 4096, "cache_size": 4,
                    "trace": "uniform", "parallelism": f"systems sharded over {world} GPU(s)"},
-        "roofline": _roof(), "valu_issue": {"frac": 0.5012345}, "valu_issue_note": None,
+        "roofline": _roof(), "valu_issue": {"frac": 0.5012345, "issue_slots": {"busy_frac": 0.855069},
+                                            "lds_bank_conflict_frac": 0.266098, "waves_per_cu": 17.61846},
+        "valu_issue_note": None,
         "kernel_fingerprint": "da9f04138f4f822f",
         "cpu_baseline": _cpu(), "cpu_baseline_mode_b": _cpu(instances=1),
         "cpu_baseline_note": "n" * 400 if with_all else None, "cpu_port": _cpu("port"),
@@ -90,7 +92,7 @@ def test_worst_case_line_fits_the_budget(world, tmp_path, capsys):
     # nothing was dropped to make it fit
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "contention", "sweep", "next",
-              "box", "rccl_world", "backend", "kernel_ms_rank", "ub_frac", "detail"):
+              "box", "rccl_world", "backend", "kernel_ms_rank", "ub_frac", "issue", "detail"):
         assert k in line, k
     assert set(line["roofline"]) == {"bound", "achieved", "peak", "unit", "frac", "traffic"}
     assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])

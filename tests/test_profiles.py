@@ -36,6 +36,30 @@ def test_profile_is_of_the_built_kernel(built_fp, name):
         f"{name} was measured on {prof.get('kernel_fingerprint')}, the built kernel is {built_fp}: refresh it"
 
 
+SWEEP = sorted(p.name for p in PROFILES.glob("pmc_sweep_cs*_p*.json"))
+
+
+@pytest.mark.parametrize("name", SWEEP)
+def test_sweep_profile_is_of_the_built_kernel(dash, name):
+    """The configs[4] point summaries (tools/evidence_sweep_pmc.sh) are bound to the first-tier kernel
+    of their CACHE_SIZE, sim_kernel<8, CS, 16, 0>: bench.py fills a sweep row's traffic only when
+    they match the library it runs."""
+    import re
+    cs = int(re.match(r"pmc_sweep_cs(\d+)_p", name).group(1))
+    prof = json.loads((PROFILES / name).read_text())
+    sym = f"_ZN4dash10sim_kernelILi8ELi{cs}ELj16ELi0EEEvNS_7SimArgsE"
+    assert prof["kernel_fingerprint"] == kf.fingerprint(LIB, sym), f"{name}: refresh it"
+    assert f"sim_kernel<8, {cs}, 16u, 0>" == prof["kernel"]
+    read = prof["tcc_ea0_rdreq_128b_sum"] * 128 + prof["tcc_ea0_rdreq_64b_sum"] * 64 + prof["tcc_ea0_rdreq_32b_sum"] * 32
+    assert read + prof["write_size"] * 1024 == pytest.approx(prof["hbm_bytes_per_launch"])
+    assert 8 < prof["waves_per_cu"] <= 18.05 and prof["wave_rounds"] > 0
+
+
+def test_sweep_covers_the_four_accounted_points():
+    assert {"pmc_sweep_cs1_p0.json", "pmc_sweep_cs4_p0.json", "pmc_sweep_cs8_p0.json",
+            "pmc_sweep_cs16_p0.json"} <= set(SWEEP)
+
+
 @pytest.mark.parametrize("kind", ["uniform", "contention"])
 def test_traffic_rederives_from_the_committed_counters(kind):
     p = json.loads((PROFILES / f"pmc_{kind}.json").read_text())

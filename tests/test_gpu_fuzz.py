@@ -23,6 +23,8 @@ pytestmark = pytest.mark.gpu
 CASES = int(os.environ.get("DASH_FUZZ_CASES", "32"))
 BASE = int(os.environ.get("DASH_FUZZ_BASE", "1000"))
 MAXLEN = int(os.environ.get("DASH_FUZZ_MAXLEN", "600"))
+# DASH_FUZZ_CS pins CACHE_SIZE (a campaign on one kernel, e.g. 8 after a change to it)
+FIX_CS = int(os.environ.get("DASH_FUZZ_CS", "0"))
 NSYS = 2048
 
 
@@ -31,6 +33,7 @@ def test_fuzz_batch_matches_oracle(dash, case):
     rng = np.random.default_rng(BASE + case)
     N = int(rng.integers(1, 9))
     CS = int(rng.integers(1, 17))
+    CS = FIX_CS or CS
     L = int(rng.integers(1, MAXLEN + 1))
     span = int(rng.choice([4, 16]))
     hot = float(rng.choice([0.0, 0.0, 0.5, 0.9]))
@@ -54,3 +57,22 @@ def test_fuzz_batch_matches_oracle(dash, case):
             hist += np.array(list(res.hist), dtype=np.uint64)
     assert stats["hist"] == hist.tolist()
     assert stats["systems"] == NSYS and stats["instructions"] == int(lens.sum())
+
+
+@pytest.mark.parametrize("N,seed", [(8, 0), (8, 0x5EED), (5, 0), (4, 0), (3, 77), (2, 0), (1, 0)])
+def test_cache_size_8_window_matches_oracle(dash, N, seed):
+    """Round 5 gave the CACHE_SIZE 8 kernel a 2-instruction trace window (two refill points per
+    4-round trip): every node count it serves (P = 1..8 lanes), long ragged traces
+    (many window wraps, lengths that end mid-chunk), lockstep and seeded, bit-exact."""
+    rng = np.random.default_rng(8000 + 10 * N + (seed & 7))
+    L = 1500
+    packed, lens = random_batch(rng, 512, N, L, block_span=16, hot_frac=0.3)
+    with dash.Engine(512, num_procs=N, cache_size=8, max_instr=L, schedule_seed=seed) as eng:
+        eng.load_traces(packed, lens)
+        stats = eng.run()
+        dig, rnd, err = eng.read_results()
+    for s in range(512):
+        res = run_system(packed[s], lens[s], num_procs=N, cache_size=8, ring_depth=256,
+                         max_rounds=1024 + 256 * L, arb_seed=seed)
+        assert (int(dig[s]), int(rnd[s]), int(err[s])) == (res.digest, res.rounds, res.errors), (N, seed, s)
+    assert stats["instructions"] == int(lens.sum())

@@ -1,19 +1,24 @@
 #!/bin/bash
-# rocprofv3 PMC passes for configs[4] sweep points: the full-size locality
-# workload at one (CACHE_SIZE, locality) point per bench run, one counter group per rocprofv3 run
-# (separate --pmc passes, each under its own time limit), then tools/pmc_summary.py per point.
-# Usage: tools/evidence_sweep_pmc.sh TAG "CS:P CS:P ..."   -> gpurun_out/sw_TAG/cs<CS>_p<P>/
+# rocprofv3 PMC passes, one counter group per rocprofv3 run (separate --pmc passes, each under its
+# own time limit), each pass's bench record in its own side file (DIR.detail.json) for
+# tools/pmc_summary.py. Points: "CS:P" = a configs[4] point (full-size locality traces at that
+# CACHE_SIZE and locality), "uniform" / "contention" = BASELINE configs[2] / [3].
+# Usage: tools/evidence_sweep_pmc.sh TAG "CS:P ... uniform contention"  -> gpurun_out/sw_TAG/<point>/
 set -uo pipefail
 TAG=$1; POINTS=${2:-"16:0 1:0 4:0 8:0"}
 OUT=gpurun_out/sw_$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
 for pt in $POINTS; do
-  cs=${pt%%:*}; p=${pt##*:}; D="$OUT/cs${cs}_p${p}"; mkdir -p "$D"
+  case "$pt" in
+    uniform|contention) D="$OUT/pmc_$pt"; ARGS="--kind $pt" ;;
+    *) cs=${pt%%:*}; p=${pt##*:}; D="$OUT/cs${cs}_p${p}"; ARGS="--kind locality --locality $p --cache-size $cs" ;;
+  esac
+  mkdir -p "$D"
   pass() {  # name counters...
     local name=$1; shift
-    step "cs $cs p $p pass $name"
+    step "$pt pass $name"
     timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-trace --output-format csv -d "$D/$name" -o run -- \
-        python3 bench.py --kind locality --locality "$p" --cache-size "$cs" --steps 1 --warmup 0 \
+        python3 bench.py $ARGS --steps 1 --warmup 0 \
         --no-cpu-baseline --contention-steps 0 --line-sweep off --line-next off --detail "$D/$name.detail.json" \
         > "$D/$name.log" 2>&1 || { echo "pass $name failed"; exit 1; }
   }

@@ -13,7 +13,9 @@ REPLY_ID fan-out share (the cold INV loop) explains where the ext
 the larger caches come from: P(a wave pops any REPLY_ID in a round) = 1 - (1 - p)^64 with p the
 REPLY_ID pops per lane-round.
 
-Usage: python3 tools/sweep_account.py [--json out.json]
+Usage: python3 tools/sweep_account.py [--dir DIR] [--json out.json]   (DIR holds the summaries; default
+profiles/, the final library's; profiles/r05/pmc_sweep/summaries_before_fanout/ holds round 5's first
+measurements, before the INV fan-out change)
 """
 import json
 import pathlib
@@ -24,8 +26,8 @@ PER_INSTR = 0.0045
 OCC = {18: 1.0, 16: 653.0 / 613.6}
 
 
-def point(cs):
-    prof = json.loads((ROOT / "profiles" / f"pmc_sweep_cs{cs}_p0.json").read_text())
+def point(cs, d):
+    prof = json.loads((d / f"pmc_sweep_cs{cs}_p0.json").read_text())
     src = ROOT / prof["source"].split()[0].rstrip("/")
     line = json.loads([x for x in pathlib.Path(str(src) + ".log").read_text().splitlines() if x.startswith("{")][-1])
     if "totals" not in line:  # round-5 compact line: the pass's side file holds the record
@@ -44,7 +46,8 @@ def point(cs):
 
 
 def main():
-    pts = {cs: point(cs) for cs in (1, 4, 8, 16)}
+    d = pathlib.Path(sys.argv[sys.argv.index("--dir") + 1]) if "--dir" in sys.argv else ROOT / "profiles"
+    pts = {cs: point(cs, d if d.is_absolute() else ROOT / d) for cs in (1, 4, 8, 16)}
     base = pts[4]
     rows = []
     for cs, p in pts.items():

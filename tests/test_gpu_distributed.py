@@ -142,3 +142,29 @@ def test_two_rank_line_sweep_matches_one_process():
         assert p2["instructions"] == 1024 * 8 * 256
         assert abs(p2["value"] - 1024 * 8 * 256 / (p2["ms_per_step"] / 1e3)) < 1e-6 * p2["value"]
     assert "not this workload" in s2["golden"]["note"]
+
+
+def test_four_ranks_line_is_the_driver_shape():
+    """The 1/2/4/8-GPU lines the driver reads (SCALE) at four ranks, rehearsed on the box's one GPU
+    over gloo: the printed line stays within 4 KB with the sweep rows in it, records the world the
+    ranks formed and the per-rank kernel spread, and its totals (headline and every sweep point)
+    equal one process running all the systems."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    small = ["--len", "256", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--contention-steps", "1",
+             "--line-sweep", "on", "--line-sweep-warmup", "0"]
+    four = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--dist-backend", "gloo",
+                           "--systems", "256"] + small, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert four.returncode == 0, four.stderr[-3000:]
+    d4 = _line(four.stdout)
+    one = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--systems", "1024"] + small,
+                         capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-3000:]
+    d1 = _line(one.stdout)
+    line = d4["_line"]
+    assert line["n_gpus"] == 4 and line["rccl_world"] == 4 and line["backend"] == "gloo"
+    lo, hi = line["kernel_ms_rank"]
+    assert 0 < lo <= hi and len(line["sweep"]["rows"]) == 25
+    assert d4["totals"] == d1["totals"] and d4["contention"]["totals"] == d1["contention"]["totals"]
+    keys = ("hist", "instructions", "rounds_total", "err_systems", "dropped", "digest_sum")
+    for p4, p1 in zip(d4["sweep"]["points"], d1["sweep"]["points"]):
+        assert {k: p4[k] for k in keys} == {k: p1[k] for k in keys}, (p4["cache_size"], p4["locality"])

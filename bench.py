@@ -1179,6 +1179,10 @@ def main():
             "valu_issue": valu_issue(prof, stats["wave_rounds"]),
             "valu_issue_note": prof_note,
             "kernel_fingerprint": fp,
+            # the first-tier kernel of this run's CACHE_SIZE, as run (tools/pmc_summary.py binds the PMC
+            # passes of this process to it, not to whatever library is built when it summarises them)
+            "kernel_fingerprint_run": (fp if args.cache_size == 4 else
+                                       kernel_fingerprint(dash.LIB_PATH, sim_symbol(args.cache_size))),
             "cpu_baseline": cpu,
             "cpu_baseline_mode_b": cpu_b,
             "cpu_baseline_note": note,

@@ -142,3 +142,21 @@ def test_committed_line_ub_frac_matches_the_oracle(path):
     assert line["ub_frac"] == pytest.approx(GOLD["uniform"]["err_systems"] / GOLD["systems"], rel=1e-2)
     assert line["contention"]["err_systems"] == GOLD["contention"]["err_systems"]
     assert line["contention"]["digest_sum"] == GOLD["contention"]["digest_sum"]
+
+
+def test_committed_line_has_every_row_measured():
+    """The committed round-5 line (the driver's command on the final library): every sweep row with
+    its value, roofline fraction, HBM traffic from that point's committed PMC passes, the reference
+    per CACHE_SIZE with at least three batches, and the three full-size golden points bit-exact."""
+    f = ROOT / "profiles" / "r05" / "bench_headline.json"
+    if not f.exists():
+        pytest.skip("not committed yet")
+    line = json.loads([x for x in f.read_text().splitlines() if x.startswith("{")][-1])
+    sw = line["sweep"]
+    cols = sw["cols"]
+    assert len(sw["rows"]) == 25
+    for row in sw["rows"]:
+        r = dict(zip(cols, row))
+        assert r["value_G"] > 0 and 0 < r["frac"] < 1 and r["traffic_GB"] and r["vs_baseline"], row
+    assert all(v[0] >= 3 for v in sw["cpu"].values()) and sw["golden_bit_exact"] == [True, True, True]
+    assert line["roofline"]["traffic"] and line["issue"]["waves_per_cu"] > 17

@@ -1,14 +1,18 @@
-"""Full-size golden totals for three points of BASELINE.json configs[4] (the CACHE_SIZE x
+"""Full-size golden totals for five points of BASELINE.json configs[4] (the CACHE_SIZE x
 locality sweep): the oracle (oracle/dash_oracle.c, test infrastructure) run over ALL 2^20
 systems x 8 nodes x 4096 instructions of the locality generator, seed 0x5EED, at
   CACHE_SIZE 1, locality 0.0;  CACHE_SIZE 4, locality 0.5;  CACHE_SIZE 16, locality 1.0
-(the corners and the middle of the grid). Writes tests/golden/sweep_full.json: per point the
+(the corners and the middle of the grid; round 4) and, since round 5, CACHE_SIZE 8, locality 0.0
+and CACHE_SIZE 16, locality 0.25 (the kernels round 5 changed: the 2-instruction trace window at
+CACHE_SIZE 8, the INV fan-out everywhere; 16 / 0.25 has the most REPLY_ID fan-outs and the most
+systems on the reference's undefined paths). Writes tests/golden/sweep_full.json: per point the
 per-type histogram, instruction / round / error-system totals and bench.digest_sum of the
 per-system digests, so the `sweep` object of the default bench.py line (1M systems per GPU
 per point) is checked bit-exactly against the oracle: tests/test_full_size_golden.py
 (committed lines) and tests/test_gpu_sweep.py (live, on the GPU box).
 
-Usage: python tests/golden/make_sweep_full.py [threads]   (about 10 min per point on 8 threads)
+Usage: python tests/golden/make_sweep_full.py [threads] [CS:P ...]   (about 10 min per point on 8
+threads; with points given, only those are computed and merged into the existing file)
 """
 import json
 import pathlib
@@ -24,7 +28,7 @@ import bench  # noqa: E402  (digest_sum)
 import oracle_ctypes as oc  # noqa: E402
 
 SYSTEMS, LEN, SEED, CHUNK = 1 << 20, 4096, 0x5EED, 1 << 15
-POINTS = [(1, 0.0), (4, 0.5), (16, 1.0)]
+POINTS = [(1, 0.0), (4, 0.5), (16, 1.0), (8, 0.0), (16, 0.25)]
 
 
 def totals(cs, p, threads):
@@ -49,9 +53,15 @@ def totals(cs, p, threads):
 
 if __name__ == "__main__":
     threads = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    only = [(int(a.split(":")[0]), float(a.split(":")[1])) for a in sys.argv[2:]]
+    path = pathlib.Path(__file__).resolve().parent / "sweep_full.json"
     out = {"systems": SYSTEMS, "num_procs": 8, "instr_per_node": LEN, "seed": SEED, "generator":
            "oracle/dash_oracle.c orc_run_batch, locality kind (counter-based, keyed by global system id)",
-           "points": [totals(cs, p, threads) for cs, p in POINTS]}
-    path = pathlib.Path(__file__).resolve().parent / "sweep_full.json"
+           "points": []}
+    if only and path.exists():
+        out = json.loads(path.read_text())
+    for cs, p in (only or POINTS):
+        pt = totals(cs, p, threads)
+        out["points"] = [q for q in out["points"] if (q["cache_size"], q["locality"]) != (cs, p)] + [pt]
     path.write_text(json.dumps(out, indent=1) + "\n")
     print(f"wrote {path}")

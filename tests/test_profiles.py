@@ -71,10 +71,10 @@ def test_traffic_rederives_from_the_committed_counters(kind):
 
 
 def test_uniform_kernel_stats_agree_with_the_pmc_run():
-    """profiles/r05/ev5_c/kernel_stats_uniform.csv: rocprofv3 --kernel-trace --stats of the bench
+    """profiles/r05/ev5_d/kernel_stats_uniform.csv: rocprofv3 --kernel-trace --stats of the bench
     command with the contention leg off (tools/evidence_r5.sh), so its sim_kernel<8,4,16,0> average
     is the headline kernel's, on the library the PMC summary measured."""
-    rows = list(csv.DictReader((PROFILES / "r05" / "ev5_c" / "kernel_stats_uniform.csv").open()))
+    rows = list(csv.DictReader((PROFILES / "r05" / "ev5_d" / "kernel_stats_uniform.csv").open()))
     row = next(r for r in rows if any(k in r["Name"] for k in ("sim_kernel<8, 4, 16u, false>", "sim_kernel<8, 4, 16u, 0>")))
     avg_ms = float(row["AverageNs"]) / 1e6
     pmc = json.loads((PROFILES / "pmc_uniform.json").read_text())

@@ -28,7 +28,7 @@ import bench  # noqa: E402  (digest_sum)
 import oracle_ctypes as oc  # noqa: E402
 
 SYSTEMS, LEN, SEED, CHUNK = 1 << 20, 4096, 0x5EED, 1 << 15
-POINTS = [(1, 0.0), (4, 0.5), (16, 1.0), (8, 0.0), (16, 0.25)]
+POINTS = [(1, 0.0), (4, 0.5), (16, 1.0), (8, 0.0), (16, 0.25)]  # the default set; more are added by CS:P
 
 
 def totals(cs, p, threads):
@@ -63,5 +63,5 @@ if __name__ == "__main__":
     for cs, p in (only or POINTS):
         pt = totals(cs, p, threads)
         out["points"] = [q for q in out["points"] if (q["cache_size"], q["locality"]) != (cs, p)] + [pt]
-    path.write_text(json.dumps(out, indent=1) + "\n")
-    print(f"wrote {path}")
+        path.write_text(json.dumps(out, indent=1) + "\n")  # after every point: a long run keeps what it did
+        print(f"wrote {path} ({len(out['points'])} points)", flush=True)

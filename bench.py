@@ -919,8 +919,14 @@ def emit(detail, detail_arg, compact=None):
     line = (compact or compact_headline)(detail, shown)
     text = json.dumps(line, separators=(",", ":"))
     if len(text) > LINE_BUDGET:  # never silently: drop the least important summaries until it fits
-        for k in ("next", "box", "cpu_baseline_mode_b", "contention"):
-            line.pop(k, None)
+        for k in ("next", "box", "cpu_baseline_mode_b", "contention", "sweep"):
+            if k == "sweep" and line.get("sweep"):  # last resort: the rows stay in the side file only
+                sw = line["sweep"]
+                vals = [r[2] for r in sw["rows"] if r[2] is not None]
+                line["sweep"] = {"rows": len(sw["rows"]), "value_G_range": [min(vals), max(vals)] if vals else None,
+                                 "golden_bit_exact": sw.get("golden_bit_exact")}
+            else:
+                line.pop(k, None)
             line["dropped_for_size"] = line.get("dropped_for_size", []) + [k]
             text = json.dumps(line, separators=(",", ":"))
             if len(text) <= LINE_BUDGET:

@@ -125,6 +125,13 @@ def test_oversized_line_drops_summaries_not_the_headline(capsys, tmp_path, monke
     bench.emit(synthetic_detail(8), str(tmp_path / "d.json"))
     line = json.loads(capsys.readouterr().out)
     assert {"value", "roofline", "cpu_baseline", "sweep"} <= set(line)
+    # a budget the sweep rows cannot fit: they stay in the side file, the line says so and still fits
+    monkeypatch.setattr(bench, "LINE_BUDGET", 1800)
+    bench.emit(synthetic_detail(8), str(tmp_path / "d.json"))
+    out = capsys.readouterr().out
+    line = json.loads(out)
+    assert len(out.strip()) <= 1800 and line["sweep"]["rows"] == 25 and "sweep" in line["dropped_for_size"]
+    assert {"value", "ms_per_step", "roofline", "cpu_baseline", "detail"} <= set(line)
 
 
 GOLD = json.loads((ROOT / "tests" / "golden" / "full_size.json").read_text())

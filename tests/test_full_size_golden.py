@@ -65,7 +65,8 @@ def _sweep_points(path):
 @pytest.mark.parametrize("path", ["profiles/r03/final/sweep.json", "profiles/r04/bench_headline.json",
                                   "profiles/r05/ev5_b/bench_detail.json",
                                   "profiles/r05/ev5_c/bench_detail.json",
-                                  "profiles/r05/ev5_d/bench_detail.json"])
+                                  "profiles/r05/ev5_d/bench_detail.json",
+                                  "profiles/r05/ev5_e/bench_detail.json"])
 def test_committed_sweep_points_match_oracle_full_size(path):
     """configs[4] at full size: three grid points of the committed GPU lines --
     round 3's `bench.py --sweep`, round 4's default headline line and round 5's side file of the

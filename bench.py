@@ -121,6 +121,54 @@ def ref_exe(cache_size):
     return ROOT / "oracle" / "_ref" / name
 
 
+WRITEBACK_INV, WRITEBACK_INT = 7, 8  # message types whose receiver comes from __builtin_ctz (ref :209,451)
+STALL_EXPLAINED = ("ctz0_send", "queue_full")
+
+
+def stall_cause(stderr_text, num_procs=8):
+    """Why a killed reference instance stalled, from its own stderr (oracle/patch_ref.py patch 5):
+    "ctz0_send" = it dropped a WRITEBACK_INT / WRITEBACK_INV addressed to a node >= NUM_PROCS other
+    than 15 -- the reference's __builtin_ctz(0) (tzcnt gives 32; ref :209,451), after which that
+    request's requester waits forever; "queue_full" = a full queue dropped a message (ref :758-762;
+    at 256 the consumer's head != tail test also stops draining, ref :167-170); "oob_evict_only" =
+    only the 0xFF-line evictions to node 15 were dropped (ref :772,786; nobody waits on those);
+    "none_logged" = no drop at all."""
+    cause = "none_logged"
+    for ln in stderr_text.splitlines():
+        f = ln.split()
+        if ln.startswith("bench: queue full"):
+            return "queue_full"
+        if ln.startswith("bench: dropped") and len(f) >= 6:
+            t, r = int(f[2]), int(f[5])
+            if t in (WRITEBACK_INV, WRITEBACK_INT) and r >= num_procs and r != 15:
+                cause = "ctz0_send"
+            elif cause == "none_logged":
+                cause = "oob_evict_only"
+    return cause
+
+
+def explain_stalls(stalls, seed, kind_id, locality, cache_size, length):
+    """every killed instance with its system id and cause (stall_cause), and the
+    oracle's lockstep verdict on that system (its error bits: DASH_ERR_CTZ0 = 4, DEADLOCK = 8 ...).
+    `explained` counts the stalls whose own log shows a send that leaves a requester waiting forever
+    (or a full queue)."""
+    from collections import Counter
+    if not stalls:
+        return {"n": 0, "explained": 0}
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_ctypes as oc
+    by_sys = Counter(i for i, _ in stalls)
+    flags = {i: int(oc.run_batch(seed, i, 1, num_procs=8, cache_size=cache_size, length=length, kind=kind_id,
+                                 locality=locality)["errors"][0]) for i in by_sys}
+    return {"n": len(stalls), "explained": sum(c in STALL_EXPLAINED for _, c in stalls),
+            "causes": dict(Counter(c for _, c in stalls)),
+            # system id -> [times it stalled, the oracle's error bits for it under lockstep]
+            "systems": {str(i): [n, flags[i]] for i, n in sorted(by_sys.items())},
+            "oracle_ctz0": sum(n for i, n in by_sys.items() if flags[i] & ERR_CTZ0),
+            "basis": "cause from the instance's own stderr (oracle/patch_ref.py patch 5); the oracle runs the "
+                     "same system under the engine's lockstep schedule"}
+
+
 def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, locality=0, kind_name=None,
                  min_batches=1):
     """The reference itself (oracle/_ref/cache_simulator_bench[_cs<C>]: assignment.c with the
@@ -160,8 +208,11 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
         # counted: instructions and time are those of the instances that finished.
         batches, hung, instr, elapsed, t0 = 0, 0, 0, 0.0, time.perf_counter()
         rates = []  # per batch: finished instances' instructions / the batch's slowest finisher
+        stalls = []  # per killed instance: (system id, cause from its own stderr)
         while True:
-            procs = [subprocess.Popen([str(exe), "b"], cwd=d, stdout=subprocess.DEVNULL) for d in dirs]
+            errs = [open(d / "stderr.txt", "w") for d in dirs]
+            procs = [subprocess.Popen([str(exe), "b"], cwd=d, stdout=subprocess.DEVNULL, stderr=f)
+                     for d, f in zip(dirs, errs)]
             tb = last = time.perf_counter()
             fin = {}
             try:
@@ -186,6 +237,9 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
                     if p.poll() is None:
                         p.kill()
                     p.wait()
+                for f in errs:
+                    f.close()
+            stalls += [(i, stall_cause((dirs[i] / "stderr.txt").read_text())) for i in range(k) if i not in fin]
             if not fin:
                 raise RuntimeError(f"no reference instance finished within {args.ref_timeout:.0f} s")
             for i in fin:  # the instance reached quiescence and dumped its 8 nodes
@@ -198,7 +252,9 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
                 break
     cores = host_cores()
     loc = f", locality {locality / 65536:g}" if kind_name == "locality" else ""
+    stalled = explain_stalls(stalls, seed, kind_id, locality, cache_size, args.len)
     return {"value": instr / elapsed, "unit": "instr/s", "cores": cores, "host_cpus_visible": host_cpus_visible(),
+            "stalled": stalled,
             "kind": "reference", "mode": "A" if k == cores else ("B" if k == 1 else f"{k} instances"),
             # spread over the batches (the spinning instances vary from batch to batch): instr/s
             "batches": {"n": len(rates), "min": min(rates), "median": sorted(rates)[len(rates) // 2],
@@ -206,7 +262,8 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
             "instances": k, "threads_per_instance": 8, "hung_instances_killed": hung, "cpu_model": cpu_model(),
             "sample": f"{batches} batch(es) x {k} concurrent instance(s) x 8 OpenMP threads, one 8-node system "
                       f"x {args.len} instr each ({kind_name}{loc}, CS={cache_size}, systems 0..{k - 1} of seed "
-                      f"0x{seed:X}) in {elapsed:.1f} s ({hung} stalled instance(s) killed, not counted); {cores} "
+                      f"0x{seed:X}) in {elapsed:.1f} s ({hung} stalled instance(s) killed, not counted: the "
+                      f"figure is over the instances that finished, see `stalled` for why the others stalled); {cores} "
                       f"CPUs of cgroup quota on a host exposing "
                       f"{host_cpus_visible()} logical CPUs ({cpu_model()}); assignment.c + benchmark patch "
                       f"(oracle/patch_ref.py), gcc -O2 -fopenmp"}
@@ -356,6 +413,89 @@ def digest_sum(digests):
     return [int((d & np.uint64(0xFFFFFFFF)).sum(dtype=np.uint64)), int((d >> np.uint64(32)).sum(dtype=np.uint64))]
 
 
+GOLDEN = ROOT / "tests" / "golden"
+_golden_cache = {}
+ERR_OOB, ERR_CTZ0 = 2, 4  # include/dash.h: the reference's undefined sends (ref :772,786 / :209,451)
+
+
+def golden_file(name):
+    """A committed golden fixture (tests/golden/<name>; data, not the oracle), or None."""
+    if name not in _golden_cache:
+        try:
+            _golden_cache[name] = json.loads((GOLDEN / name).read_text())
+        except (OSError, ValueError):
+            _golden_cache[name] = None
+    return _golden_cache[name]
+
+
+def golden_key(kind_name, cache_size, locality=None):
+    """The workload's key in the golden fixtures: "uniform" / "contention" (CACHE_SIZE 4) or
+    "locality:<CS>:<p>" (the configs[4] grid)."""
+    return kind_name if kind_name in ("uniform", "contention") else f"locality:{cache_size}:{locality:g}"
+
+
+def slice_golden(key, cache_size, local, sys_base, M, args):
+    """This rank's own (pre-reduce) totals against the oracle's full-size totals of global systems
+    [0, 2^20): tests/golden/full_size.json (uniform, contention) and sweep_full.json (configs[4]).
+    True / False when this rank owns exactly that slice and a golden exists for the workload, else
+    None. At any GPU count rank 0 owns [0, 2^20) (shard()), so every driver line is checked."""
+    if sys_base != 0:
+        return None
+    if key in ("uniform", "contention"):
+        g = golden_file("full_size.json")
+        gp = g.get(key) if g and g.get("cache_size") == cache_size else None
+    else:
+        g = golden_file("sweep_full.json")
+        gp = next((q for q in (g or {}).get("points", []) if golden_key("locality", q["cache_size"], q["locality"])
+                   == key), None)
+    if not gp or (g["systems"], g["instr_per_node"], g["seed"]) != (M, args.len, args.seed):
+        return None
+    return all(local[k] == gp[k] for k in ("hist", "instructions", "rounds_total", "err_systems", "digest_sum"))
+
+
+def sample_check(key, cache_size, sys_base, M, args, digests, rounds, errors):
+    """Every rank: its systems among the sampled global ids of tests/golden/rank_samples.json
+    (make_rank_samples.py) against the oracle's per-system digest, rounds and error bits.
+    Returns (checked, mismatched)."""
+    s = golden_file("rank_samples.json")
+    w = (s or {}).get("workloads", {}).get(key)
+    if not w or w["cache_size"] != cache_size or (s["seed"], s["instr_per_node"]) != (args.seed, args.len):
+        return 0, 0
+    checked = bad = 0
+    for i, g in enumerate(s["ids"]):
+        if sys_base <= g < sys_base + M:
+            j = g - sys_base
+            checked += 1
+            bad += (int(digests[j]) != int(w["digest"][i], 16) or int(rounds[j]) != w["rounds"][i]
+                    or int(errors[j]) != w["errors"][i])
+    return checked, bad
+
+
+# the all-reduced counter vector of one workload: hist[13], instructions, rounds_total, err_systems,
+# dropped, digest_sum[2], ub_systems, sampled systems checked, sampled mismatches, ranks with samples
+N_COUNTERS = 23
+
+
+def local_totals(eng, stats, key, cache_size, sys_base, M, args):
+    """After a timed region: this rank's counter vector (above) and its slice check (slice_golden).
+    Reads the per-system results once (digests, rounds, error bits)."""
+    d, r, e = eng.read_results()
+    dsum = digest_sum(d)
+    local = {"hist": stats["hist"], "instructions": stats["instructions"], "rounds_total": stats["rounds_total"],
+             "err_systems": stats["err_systems"], "digest_sum": dsum}
+    ub = int(((e & (ERR_OOB | ERR_CTZ0)) != 0).sum())
+    checked, bad = sample_check(key, cache_size, sys_base, M, args, d, r, e)
+    vec = (stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"], stats["dropped"]]
+           + dsum + [ub, checked, bad, 1 if checked else 0])
+    return vec, slice_golden(key, cache_size, local, sys_base, M, args)
+
+
+def samples_obj(totals, world):
+    """The sampled-id check summed over the ranks: systems checked, mismatches, ranks that held
+    samples (all of them when the ranks' slices are 2^20 systems or a few hundred)."""
+    return {"checked": totals[20], "mismatched": totals[21], "ranks": totals[22], "world": world}
+
+
 def sim_symbol(cache_size):
     """Mangled name of the first-tier lockstep kernel sim_kernel<8, CS, 16, 0> (8-node systems)."""
     return f"_ZN4dash10sim_kernelILi8ELi{cache_size}ELj16ELi0EEEvNS_7SimArgsE"
@@ -417,10 +557,8 @@ def sweep_gpu(args, dash, rank, world, dev, steps, warmup):
                 loc = int(round(p * 65536))
                 eng.generate(args.seed, args.len, kind=dash.GEN_LOCALITY, locality=loc, sys_base=sys_base)
                 elapsed, stats, kms = timed_headline(eng, a, world, dev)
-                dsum = digest_sum(eng.read_results()[0])
-                elapsed, totals = reduce_totals(
-                    elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
-                                              stats["dropped"]] + dsum, torch.device("cuda", dev), world)
+                vec, slice_ok = local_totals(eng, stats, golden_key("locality", cs, p), cs, sys_base, M, args)
+                elapsed, totals = reduce_totals(elapsed, vec, torch.device("cuda", dev), world)
                 avg_s = sum(kms) / len(kms) / 1e3
                 # committed PMC passes of this point (tools/evidence_sweep_pmc.sh), only for the full-size
                 # workload and only when measured on this code object
@@ -438,9 +576,14 @@ def sweep_gpu(args, dash, rank, world, dev, steps, warmup):
                                "wave_rounds": stats["wave_rounds"],
                                "hist": totals[:13], "instructions": totals[13], "rounds_total": totals[14],
                                "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19],
-                               # systems that hit the reference's undefined behaviour (DASH_ERR_OOB / CTZ0):
-                               # parity there is with the engine's defined drop rule
-                               "ub_frac": totals[15] / (world * M),
+                               # systems that hit the reference's undefined behaviour (DASH_ERR_OOB / CTZ0
+                               # only): parity there is with the engine's defined drop rule
+                               "ub_systems": totals[19], "ub_frac": totals[19] / (world * M),
+                               "err_frac": totals[15] / (world * M),
+                               # rank 0's slice [0, 2^20) against sweep_full.json; every rank's sampled ids
+                               # against rank_samples.json
+                               "golden_slice": slice_ok if rank == 0 else None,
+                               "samples": samples_obj(totals, world),
                                "tier_systems": stats["tier_systems"]})
         finally:
             eng.close()
@@ -450,27 +593,34 @@ def sweep_gpu(args, dash, rank, world, dev, steps, warmup):
 
 
 def sweep_cpu(args, dash, points, target_s, min_batches=3):
-    """The reference itself per CACHE_SIZE: mode (A), one instance per host
-    core, the binary built for that CACHE_SIZE, on systems 0.. of the locality-0.5 traces, at least
-    `min_batches` batches (and `target_s` seconds); the figure (with its batch spread and stalled
-    instances) is the `cpu_baseline` of that CACHE_SIZE's five points. Rank 0, after every GPU
-    point and after the process group is gone. Returns {cs: baseline or None}."""
+    """The reference itself on EACH point's own traces (its speed depends heavily on
+    locality, so one figure per CACHE_SIZE misstates the other localities by up to ~45x): mode (A),
+    one instance per host core, the binary built for the point's CACHE_SIZE, systems 0.. of that
+    point's locality traces, at least `min_batches` batches (and `target_s` seconds). Each point's
+    `vs_baseline` is against its own figure. Rank 0, after every GPU point and after the process
+    group is gone. Returns {cs: the five points' batches and stalled instances, summed}."""
     per_cs = {}
-    for cs in sorted({pt["cache_size"] for pt in points}):
-        per_cs[cs] = None
-        if args.no_cpu_baseline:
-            continue
-        try:
-            per_cs[cs] = ref_baseline(args, args.seed, dash.GEN_LOCALITY, target_s, args.ref_instances,
-                                      cache_size=cs, locality=32768, kind_name="locality", min_batches=min_batches)
-        except Exception as e:  # reported, never substituted by the port
-            per_cs[cs] = {"error": f"reference baseline unavailable: {e}"}
     for pt in points:
-        cpu = per_cs.get(pt["cache_size"])
+        cs = pt["cache_size"]
+        cpu = None
+        if not args.no_cpu_baseline:
+            try:
+                cpu = ref_baseline(args, args.seed, dash.GEN_LOCALITY, target_s, args.ref_instances, cache_size=cs,
+                                   locality=int(round(pt["locality"] * 65536)), kind_name="locality",
+                                   min_batches=min_batches)
+            except Exception as e:  # reported, never substituted by the port
+                cpu = {"error": f"reference baseline unavailable: {e}"}
         ok = cpu is not None and "value" in cpu
         pt["cpu_baseline"] = cpu if ok else None
         pt["vs_baseline"] = pt["value"] / cpu["value"] if ok else None
         pt["cpu_baseline_note"] = None if ok else (cpu or {}).get("error", "no CPU baseline (--no-cpu-baseline)")
+        agg = per_cs.setdefault(cs, {"points": 0, "batches": 0, "hung": 0, "hung_explained": 0, "oracle_ctz0": 0})
+        if ok:
+            agg["points"] += 1
+            agg["batches"] += cpu["batches"]["n"]
+            agg["hung"] += cpu["hung_instances_killed"]
+            agg["hung_explained"] += cpu["stalled"]["explained"]
+            agg["oracle_ctz0"] += cpu["stalled"].get("oracle_ctz0", 0)
     return per_cs
 
 
@@ -492,7 +642,7 @@ def sweep(args, dash, rank, world, dev):
                              "parallelism": f"systems sharded over {world} GPU(s)"},
                   "vs_baseline_basis": SWEEP_CPU_BASIS,
                   "sweep": {"steps": args.steps, "warmup": args.warmup, "cpu_per_cache_size": per_cs,
-                            "golden": sweep_golden_check(points, world * M, args), "points": points}}
+                            "golden": sweep_golden_summary(points, M), "points": points}}
 
         def compact(d, shown):
             out = {k: d[k] for k in ("metric", "unit", "n_gpus", "steps", "warmup", "higher_is_better",
@@ -743,40 +893,48 @@ def run_kind(dash, args, kind_name, M, sys_base, world, dev, steps, tier_flag, s
         else:
             elapsed, stats, kernel_ms = timed_headline(eng, a, world, dev)
         # a checksum of the per-system state digests (sums of their 32-bit
-        # halves: order-free, so identical for any GPU count), read back after the timed region
-        dsum = digest_sum(eng.read_results()[0])
+        # halves: order-free, so identical for any GPU count), read back after the timed region,
+        # with this rank's golden checks (its slice, its sampled ids)
+        key = golden_key(kind_name, args.cache_size, args.locality)
+        vec, slice_ok = local_totals(eng, stats, key, args.cache_size, sys_base, M, args)
     finally:
         eng.close()
-    elapsed, totals = reduce_totals(
-        elapsed, stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"],
-                                  stats["dropped"]] + dsum, torch.device("cuda", dev), world)
-    return elapsed, totals, stats, kernel_ms
+    elapsed, totals = reduce_totals(elapsed, vec, torch.device("cuda", dev), world)
+    return elapsed, totals, stats, kernel_ms, slice_ok
 
 
-def sweep_golden_check(points, systems, args):
-    """The sweep points whose full-size totals the oracle pinned (tests/golden/sweep_full.json,
-    make_sweep_full.py): equal or not, per point (a fixture file, not the oracle)."""
-    f = ROOT / "tests" / "golden" / "sweep_full.json"
-    if not f.exists():
-        return None
-    g = json.loads(f.read_text())
-    if (g["systems"], g["instr_per_node"], g["seed"]) != (systems, args.len, args.seed):
-        return {"note": "golden is for 2^20 systems x 4096 instr, seed 0x5EED: not this workload"}
-    out = []
-    for gp in g["points"]:
-        pt = next((p for p in points if (p["cache_size"], p["locality"]) == (gp["cache_size"], gp["locality"])), None)
-        if pt is None:
-            continue
-        same = (pt["hist"] == gp["hist"] and pt["instructions"] == gp["instructions"] and
-                pt["rounds_total"] == gp["rounds_total"] and pt["err_systems"] == gp["err_systems"] and
-                pt["digest_sum"] == gp["digest_sum"])
-        out.append({"cache_size": gp["cache_size"], "locality": gp["locality"], "bit_exact": same})
-    return out
+def sweep_golden_summary(points, M):
+    """The sweep's golden checks per point (labelled): rank 0's slice against sweep_full.json
+    (null where no full-size golden exists for this workload) and the sampled ids of every rank."""
+    return {"slice": [0, M], "slice_basis": "rank 0's own totals of global systems [0, M) vs "
+                                            "tests/golden/sweep_full.json (oracle, 2^20 systems x 4096 instr)",
+            "points": [{"cache_size": p["cache_size"], "locality": p["locality"], "bit_exact": p["golden_slice"],
+                        "samples": p["samples"]} for p in points]}
 
 
-def totals_dict(totals):
+def golden_record(slice_ok, cont, points, totals, world, M):
+    """The line's `golden` object: rank 0's slice [0, M) against the full-size goldens (headline,
+    contention, and how many of the sweep points that have one are bit-exact: [equal, with a golden,
+    points]), and the sampled ids summed over every workload of the run: [checked, mismatched, the
+    fewest ranks holding samples in any workload, world]."""
+    objs = [samples_obj(totals, world)] + ([cont["totals"]["samples"]] if cont else []) + \
+        [p["samples"] for p in points or []]
+    flags = [p["golden_slice"] for p in points] if points else None
+    return {"slice": [0, M], "headline": slice_ok, "contention": cont.get("golden_slice") if cont else None,
+            "sweep": ([sum(f is True for f in flags), sum(f is not None for f in flags), len(flags)]
+                      if flags is not None else None),
+            "samples": [sum(o["checked"] for o in objs), sum(o["mismatched"] for o in objs),
+                        min(o["ranks"] for o in objs), world],
+            "basis": "slice: rank 0's own pre-reduce totals (hist, instructions, rounds, err_systems, digest_sum) vs "
+                     "tests/golden/full_size.json / sweep_full.json, null where no golden covers the workload; samples: "
+                     "each rank's systems among tests/golden/rank_samples.json's ids, per-system digest + rounds + "
+                     "error bits"}
+
+
+def totals_dict(totals, world=1):
     return {"hist": totals[:13], "instructions_per_step": totals[13], "rounds_total": totals[14],
-            "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19]}
+            "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19],
+            "ub_systems": totals[19], "samples": samples_obj(totals, world)}
 
 
 def rank_spread(x, device):
@@ -793,8 +951,8 @@ def rank_spread(x, device):
     return [float(lo.item()), float(hi.item())]
 
 
-SWEEP_CPU_BASIS = ("per CACHE_SIZE: the reference built for it, mode (A), >= 3 batches on systems 0.. of the "
-                   "locality-0.5 traces; that figure is the cpu_baseline of the CACHE_SIZE's five points")
+SWEEP_CPU_BASIS = ("per point: the reference built for its CACHE_SIZE, mode (A), >= 3 batches on systems 0.. of "
+                   "that point's own locality traces; each point's vs_baseline is against its own figure")
 
 
 def sig(x, n=4):
@@ -817,6 +975,7 @@ def compact_cpu(c, sample=True):
         out["batches"] = [b["n"], sig(b["min"], 3), sig(b["median"], 3), sig(b["max"], 3)]
     if "hung_instances_killed" in c:
         out["hung"] = c["hung_instances_killed"]
+        out["hung_explained"] = (c.get("stalled") or {}).get("explained")
     if sample:
         out["cpu_model"] = (c.get("cpu_model") or "")[:48]
         out["sample"] = ((f"{c['instances']} concurrent instances x 8 OpenMP threads, assignment.c + bench patch, "
@@ -850,6 +1009,9 @@ def compact_headline(d, detail_path):
                          "lds_conflict": sig(vi.get("lds_bank_conflict_frac"), 3),
                          "waves_per_cu": sig(vi.get("waves_per_cu"), 3)}
     line["ub_frac"] = sig(d.get("ub_frac"), 3)
+    g = d.get("golden")
+    if g:
+        line["golden"] = {k: g.get(k) for k in ("slice", "headline", "contention", "sweep", "samples")}
     line["cpu_baseline"] = compact_cpu(d.get("cpu_baseline"))
     if d.get("cpu_baseline_note"):
         line["cpu_baseline_note"] = d["cpu_baseline_note"][:160]
@@ -888,17 +1050,15 @@ def compact_sweep(sw):
     def giga(x):
         return sig(x / 1e9, 4) if x is not None else None
     rows = [[p["cache_size"], p["locality"], giga(p["value"]), sig(p["ms_per_step"]), sig(p["roofline"]["frac"], 3),
-             sig(p.get("vs_baseline"), 3), sig(p["ub_frac"], 3), giga(p["roofline"].get("traffic"))]
+             sig(p.get("vs_baseline"), 3), sig(p["ub_frac"], 3), giga(p["roofline"].get("traffic")),
+             p.get("golden_slice"), (p.get("samples") or {}).get("mismatched")]
             for p in sw["points"]]
-    cpu = {str(cs): ([c["batches"]["n"], sig(c["value"], 3), sig(c["batches"]["min"], 3),
-                      sig(c["batches"]["median"], 3), sig(c["batches"]["max"], 3), c["hung_instances_killed"]]
-                     if c and "value" in c else None)
+    cpu = {str(cs): ([c["points"], c["batches"], c["hung"], c["hung_explained"]] if c else None)
            for cs, c in (sw.get("cpu_per_cache_size") or {}).items()}
-    g = sw.get("golden")
-    return {"cols": ["cs", "p", "value_G", "ms_per_step", "frac", "vs_baseline", "ub_frac", "traffic_GB"],
+    return {"cols": ["cs", "p", "value_G", "ms_per_step", "frac", "vs_baseline", "ub_frac", "traffic_GB",
+                     "golden", "smp_bad"],
             "rows": rows, "steps": sw["steps"],
-            "cpu_cols": ["n", "value", "min", "median", "max", "hung"], "cpu": cpu,
-            "golden_bit_exact": ([x["bit_exact"] for x in g] if isinstance(g, list) else None)}
+            "cpu_cols": ["points", "batches", "hung", "hung_explained"], "cpu": cpu}
 
 
 def detail_path_arg(p):
@@ -924,7 +1084,7 @@ def emit(detail, detail_arg, compact=None):
                 sw = line["sweep"]
                 vals = [r[2] for r in sw["rows"] if r[2] is not None]
                 line["sweep"] = {"rows": len(sw["rows"]), "value_G_range": [min(vals), max(vals)] if vals else None,
-                                 "golden_bit_exact": sw.get("golden_bit_exact")}
+                                 "golden_not_exact": [[r[0], r[1]] for r in sw["rows"] if r[8] is False]}
             else:
                 line.pop(k, None)
             line["dropped_for_size"] = line.get("dropped_for_size", []) + [k]
@@ -1077,7 +1237,7 @@ def main():
     probe0 = box_probe(dash, dev)
     pdev = probe0.get("_dev") or {}
     sampler = ClockSampler(sysfs_dev_path(pdev["pci_domain"], pdev["pci_bus"])) if pdev else None
-    elapsed, totals, stats, kernel_ms = run_kind(dash, args, args.kind, M, sys_base, world, dev,
+    elapsed, totals, stats, kernel_ms, slice_ok = run_kind(dash, args, args.kind, M, sys_base, world, dev,
                                                  args.steps, tier_flag, sampler)
     probe1 = box_probe(dash, dev)
     instr_per_step = world * M * 8 * args.len
@@ -1090,7 +1250,7 @@ def main():
     # configs[3] beside the headline: its own warmup and timed steps (same barriers)
     cont = None
     if args.contention_steps > 0 and args.kind == "uniform":
-        c_el, c_tot, c_stats, c_kms = run_kind(dash, args, "contention", M, sys_base, world, dev,
+        c_el, c_tot, c_stats, c_kms, c_slice_ok = run_kind(dash, args, "contention", M, sys_base, world, dev,
                                                args.contention_steps, tier_flag)
         c_prof, c_note = read_profile("contention", fp) if full else (None, prof_note)
         c_avg = sum(c_kms) / len(c_kms) / 1e3
@@ -1103,7 +1263,7 @@ def main():
                 "roofline": roofline(M, args.len, c_avg, c_prof, c_note),
                 "valu_issue": valu_issue(c_prof, c_stats["wave_rounds"]),
                 "tier_systems": c_stats["tier_systems"], "wave_rounds": c_stats["wave_rounds"],
-                "totals": totals_dict(c_tot)}
+                "totals": totals_dict(c_tot, world), "golden_slice": c_slice_ok}
 
     # configs[4] beside the headline: the whole CACHE_SIZE x locality grid at
     # this line's systems per GPU, --line-sweep-warmup untimed and --line-sweep-steps timed steps per
@@ -1139,7 +1299,7 @@ def main():
                                      f"(BASELINE configs[4]; seed 0x{args.seed:X}, keyed by global id)",
                          "steps": args.line_sweep_steps, "warmup": args.line_sweep_warmup,
                          "cpu_baseline_basis": SWEEP_CPU_BASIS, "cpu_per_cache_size": sweep_cpu_obj,
-                         "golden": sweep_golden_check(points, world * M, args), "points": points}
+                         "golden": sweep_golden_summary(points, M), "points": points}
         cpu, cpu_b, port, note = None, None, None, None
         if not args.no_cpu_baseline:
             kind_id = {"uniform": dash.GEN_UNIFORM, "contention": dash.GEN_CONTENTION,
@@ -1202,12 +1362,18 @@ def main():
             "wave_rounds": stats["wave_rounds"],
             # systems whose run hit the reference's undefined send to node 15 (ref :772,786):
             # parity there is with the engine's defined drop-and-flag rule
-            "totals": totals_dict(totals),
-            "ub_frac": totals[15] / (world * M),
-            "parity_note": ("totals.err_systems systems hit the reference's undefined behaviour (mostly the "
-                            "send to node 15, assignment.c:772,786: DASH_ERR_OOB); on them parity is with the "
-                            "engine's defined drop-and-flag rule (DESIGN.md §2), the rest with the reference's "
-                            "semantics under the lockstep schedule"),
+            "totals": totals_dict(totals, world),
+            "ub_frac": totals[19] / (world * M),
+            "err_frac": totals[15] / (world * M),
+            # the line certifies its own results at any GPU count -- rank 0's
+            # own slice (global systems [0, M), the committed full-size goldens when M = 2^20) and
+            # every rank's sampled ids (tests/golden/rank_samples.json)
+            "golden": golden_record(slice_ok, cont, points, totals, world, M),
+            "parity_note": ("totals.ub_systems systems hit the reference's undefined behaviour (mostly the "
+                            "send to node 15, assignment.c:772,786: DASH_ERR_OOB; or ctz(0), :209,451: "
+                            "DASH_ERR_CTZ0); on them parity is with the engine's defined drop-and-flag rule "
+                            "(DESIGN.md §2), the rest with the reference's semantics under the lockstep "
+                            "schedule. err_frac also counts systems flagged only DEADLOCK / STUCK etc."),
             "contention": cont,
             "sweep": sweep_obj,
             "next": next_rows,

@@ -19,6 +19,12 @@ The patch (each edit is anchored on text that must occur exactly once):
      count of threads whose instructions are all done; a thread that has printed
      its final state (ref :632-646) exits once every thread is done and nothing
      is in flight. The unpatched program never exits (ref :165).
+  5. (round 6) the first send of each message type that patch 3 drops, and the first of each type
+     that a full queue drops (ref :758-762), is noted on stderr as
+     `bench: dropped <type> to node <receiver>` / `bench: queue full at node <receiver>, dropped
+     <type>`, so bench.py can say why an instance it killed had stalled (a WRITEBACK_INT /
+     WRITEBACK_INV sent to node 32 is the reference's __builtin_ctz(0), ref :209,451: its requester
+     then waits forever). Only the drop paths print; the handlers are untouched.
 Everything else -- the handlers, locks, spinning, state dumps -- is the reference.
 """
 import pathlib
@@ -33,7 +39,14 @@ EDITS = [
     ("omp_lock_t msgBufferLocks[ NUM_PROCS ];\n",
      "omp_lock_t msgBufferLocks[ NUM_PROCS ];\n"
      "static long bench_inflight = 0;  /* patch 4 */\n"
-     "static int bench_done = 0;\n"),
+     "static int bench_done = 0;\n"
+     "static unsigned bench_noted = 0;  /* patch 5 */\n"
+     "static void bench_note_drop( int receiver, int type, int full ) {\n"
+     "    unsigned bit = 1u << ( ( type & 15 ) + ( full ? 16 : 0 ) );\n"
+     "    if ( __atomic_fetch_or( &bench_noted, bit, __ATOMIC_SEQ_CST ) & bit ) return;\n"
+     "    if ( full ) fprintf( stderr, \"bench: queue full at node %d, dropped %d\\n\", receiver, type );\n"
+     "    else fprintf( stderr, \"bench: dropped %d to node %d\\n\", type, receiver );\n"
+     "}\n"),
     ("                messageBuffers[ threadId ].count > 0 &&",
      "                __atomic_load_n( &messageBuffers[ threadId ].count, __ATOMIC_SEQ_CST ) > 0 &&"),
     ("                messageBuffers[ threadId ].count--;\n",
@@ -57,11 +70,17 @@ EDITS = [
      "                     __atomic_load_n( &bench_inflight, __ATOMIC_SEQ_CST ) == 0 )\n"
      "                    break;\n"),
     ("    omp_set_lock( &msgBufferLocks[ receiver ] );\n",
-     "    if ( receiver < 0 || receiver >= NUM_PROCS ) return;  /* patch 3 */\n"
+     "    if ( receiver < 0 || receiver >= NUM_PROCS ) {  /* patch 3 */\n"
+     "        bench_note_drop( receiver, msg.type, 0 );\n"
+     "        return;\n"
+     "    }\n"
      "    omp_set_lock( &msgBufferLocks[ receiver ] );\n"),
     ("      buf->count++;\n",
      "      __atomic_fetch_add( &bench_inflight, 1, __ATOMIC_SEQ_CST );\n"
      "      __atomic_fetch_add( &buf->count, 1, __ATOMIC_SEQ_CST );\n"),
+    ("    } else {\n#ifdef DEBUG\n        fprintf(stderr, \"Error: Message buffer overflow",
+     "    } else {\n        bench_note_drop( receiver, msg.type, 1 );  /* patch 5 */\n"
+     "#ifdef DEBUG\n        fprintf(stderr, \"Error: Message buffer overflow"),
 ]
 
 

@@ -59,7 +59,7 @@ if __name__ == "__main__":
     out = {"systems": SYSTEMS, "num_procs": 8, "instr_per_node": LEN, "seed": SEED, "generator":
            "oracle/dash_oracle.c orc_run_batch, locality kind (counter-based, keyed by global system id)",
            "points": []}
-    if only and path.exists():
+    if path.exists():  # always merge: a run never drops points it did not compute
         out = json.loads(path.read_text())
     for cs, p in (only or POINTS):
         pt = totals(cs, p, threads)

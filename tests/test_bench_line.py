@@ -21,6 +21,8 @@ def _cpu(kind="reference", instances=16):
     return {"value": 512345.678901, "unit": "instr/s", "cores": 16, "host_cpus_visible": 256, "kind": kind,
             "mode": "A", "batches": {"n": 12, "min": 441234.5678, "median": 525678.1234, "max": 639876.54321},
             "instances": instances, "threads_per_instance": 8, "hung_instances_killed": 3,
+            "stalled": {"n": 3, "explained": 3, "causes": {"ctz0_send": 3}, "systems": {"5": [3, 12]},
+                        "oracle_ctz0": 3, "basis": "q" * 200},
             "cpu_model": "AMD EPYC 9575F 64-Core Processor with a very long model name string",
             "sample": "x" * 600}
 
@@ -42,12 +44,17 @@ def synthetic_detail(world=8, with_all=True):
                     "instructions": 34359738368 * world, "rounds_total": 24731883018 * world,
                     "err_systems": 224302 * world, "dropped": 210077 * world,
                     "digest_sum": [2251634405826991 * world, 2249834063518710 * world],
-                    "ub_frac": 0.2139053344726562, "tier_systems": [M, 12345, 67],
+                    "ub_frac": 0.2139053344726562, "tier_systems": [M, 12345, 67], "ub_systems": 224302 * world,
+                    "err_frac": 0.2139053344726562, "golden_slice": True,
+                    "samples": {"checked": 32 * world, "mismatched": 0, "ranks": world, "world": world},
                     "cpu_baseline": _cpu(), "vs_baseline": 68371.23456789, "cpu_baseline_note": None})
-    per_cs = {cs: _cpu() for cs in (1, 2, 4, 8, 16)}
+    per_cs = {cs: {"points": 5, "batches": 15, "hung": 11, "hung_explained": 11, "oracle_ctz0": 11}
+              for cs in (1, 2, 4, 8, 16)}
+    smp = {"checked": 48 * world, "mismatched": 0, "ranks": world, "world": world}
     tot = {"hist": [15438985135] * 13, "instructions_per_step": 34359738368 * world,
            "rounds_total": 23801163240 * world, "err_systems": 51391 * world, "dropped": 60000 * world,
-           "digest_sum": [2251634405826991 * world, 2249834063518710 * world]}
+           "digest_sum": [2251634405826991 * world, 2249834063518710 * world], "ub_systems": 51391 * world,
+           "samples": smp}
     probe = {"probe_ms": 163.759, "probe_valu_per_s": 839274538336.1628, "sclk_mhz": 1976.6,
              "sclk_min_mhz": 1853.2, "sclk_max_mhz": 2100.9, "sysfs": {"pci": "0000:dc:00.0", "power_w": 937.0}}
     return {
@@ -70,14 +77,15 @@ def synthetic_detail(world=8, with_all=True):
         "tier_systems": [M, 3, 0], "wave_rounds": 3018808080, "totals": tot, "ub_frac": 0.0490102767944336,
         "parity_note": "p" * 300,
         "contention": {"value": 6.78123456789e10 * world, "ms_per_step": 503.123456789, "roofline": _roof(),
-                       "totals": tot, "kernel_ms_avg": 503.0},
+                       "totals": tot, "kernel_ms_avg": 503.0, "golden_slice": True},
         "sweep": {"steps": 1, "warmup": 1, "cpu_per_cache_size": per_cs,
-                  "golden": [{"cache_size": 1, "locality": 0.0, "bit_exact": True}] * 5, "points": pts},
+                  "golden": bench.sweep_golden_summary(pts, M), "points": pts},
         "next": {"events": {"slowdown": 1.10987654, "parity_same_digests_as_fast": True,
                             "parity_events_logged": True},
                  "seeded": {"slowdown": 1.48123456, "parity_all_issued": True, "parity_reproducible": True}},
         "box": {"probe_before": probe, "probe_after": probe, "device": {"name": "AMD Instinct MI355X"}},
-    }
+    } | {"golden": bench.golden_record(True, {"totals": tot, "golden_slice": True}, pts,
+                                       tot["hist"] + [0] * 6 + [51391 * world, 48 * world, 0, world], world, M)}
 
 
 @pytest.mark.parametrize("world", [1, 8])
@@ -97,8 +105,16 @@ def test_worst_case_line_fits_the_budget(world, tmp_path, capsys):
     assert set(line["roofline"]) == {"bound", "achieved", "peak", "unit", "frac", "traffic"}
     assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])
     assert len(line["sweep"]["rows"]) == 25 and len(line["sweep"]["rows"][0]) == len(line["sweep"]["cols"])
-    assert line["sweep"]["golden_bit_exact"] == [True] * 5
-    assert all(v[0] >= 3 for v in line["sweep"]["cpu"].values())
+    # the line certifies its own results at any N -- rank 0's slice against the
+    # full-size goldens, every rank's sampled ids -- and each sweep row says which point it checked
+    g = line["golden"]
+    assert g["slice"] == [0, 1 << 20] and g["headline"] is True and g["contention"] is True
+    assert g["sweep"] == [25, 25, 25] and g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == world
+    cols = line["sweep"]["cols"]
+    assert all(dict(zip(cols, r))["golden"] is True and dict(zip(cols, r))["smp_bad"] == 0
+               for r in line["sweep"]["rows"])
+    assert all(v[1] >= 15 and v[3] == v[2] for v in line["sweep"]["cpu"].values())
+    assert line["cpu_baseline"]["hung_explained"] == line["cpu_baseline"]["hung"]
     # the side file holds the full record
     assert json.loads((long_dir / "bench_detail.json").read_text()) == json.loads(json.dumps(d))
 
@@ -112,7 +128,7 @@ def test_line_values_round_trip():
     assert line["cpu_baseline"]["value"] == pytest.approx(d["cpu_baseline"]["value"], rel=1e-3)
     row = line["sweep"]["rows"][0]
     assert row[:2] == [1, 0.0] and row[6] == pytest.approx(d["sweep"]["points"][0]["ub_frac"], rel=1e-2)
-    assert line["ub_frac"] == pytest.approx(d["totals"]["err_systems"] / (1 << 20), rel=1e-2)
+    assert line["ub_frac"] == pytest.approx(d["totals"]["ub_systems"] / (1 << 20), rel=1e-2)
 
 
 def test_sig_keeps_types():

@@ -14,7 +14,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = pathlib.Path(__file__).resolve().parent.parent
-ARGS = ["--systems", "2048", "--len", "512", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
+ARGS = ["--systems", "2048", "--len", "4096", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"]
 # the torchrun rehearsal keeps the headline workload only
 
 
@@ -53,13 +53,17 @@ def test_two_ranks_match_one_process():
     assert d2["_line"]["rccl_world"] == 2 and d2["_line"]["backend"] == "gloo"
     lo, hi = d2["_line"]["kernel_ms_rank"]
     assert 0 < lo <= hi
-    assert d2["totals"]["instructions_per_step"] == d1["totals"]["instructions_per_step"] == 4096 * 8 * 512
+    assert d2["totals"]["instructions_per_step"] == d1["totals"]["instructions_per_step"] == 4096 * 8 * 4096
     assert d2["totals"]["hist"] == d1["totals"]["hist"]
     assert d2["totals"]["rounds_total"] == d1["totals"]["rounds_total"]
     assert d2["totals"]["err_systems"] == d1["totals"]["err_systems"]
     assert d2["totals"]["digest_sum"] == d1["totals"]["digest_sum"]  # final states, order-free
+    # both ranks checked their own sampled ids against the oracle's per-system results
+    g = d2["_line"]["golden"]
+    assert g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == 2 and g["samples"][0] > 0, g
+    assert d2["totals"]["samples"]["checked"] == d1["totals"]["samples"]["checked"] > 0
     # value = all ranks' instructions / max-over-ranks time
-    assert abs(d2["value"] - 4096 * 8 * 512 / (d2["ms_per_step"] / 1e3)) < 1e-6 * d2["value"]
+    assert abs(d2["value"] - 4096 * 8 * 4096 / (d2["ms_per_step"] / 1e3)) < 1e-6 * d2["value"]
 
 
 def test_bench_spawns_two_ranks_without_torchrun():
@@ -78,7 +82,7 @@ def test_bench_spawns_two_ranks_without_torchrun():
     assert d2["rccl_world"] == 2 and d1["rccl_world"] == 1 and d1["backend"] is None
     assert d2["totals"] == d1["totals"]
     assert d2["contention"]["totals"] == d1["contention"]["totals"]
-    assert d2["contention"]["totals"]["instructions_per_step"] == 4096 * 8 * 512
+    assert d2["contention"]["totals"]["instructions_per_step"] == 4096 * 8 * 4096
 
 
 def test_multi_gpu_line_carries_the_reference_baseline():
@@ -150,7 +154,9 @@ def test_four_ranks_line_is_the_driver_shape():
     ranks formed and the per-rank kernel spread, and its totals (headline and every sweep point)
     equal one process running all the systems."""
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
-    small = ["--len", "256", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--contention-steps", "1",
+    # 4096 instructions per node: the length the golden fixtures hold, so every rank checks its
+    # sampled ids (tests/golden/rank_samples.json) in every workload (VERDICT r5 next #1)
+    small = ["--len", "4096", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--contention-steps", "1",
              "--line-sweep", "on", "--line-sweep-warmup", "0"]
     four = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--dist-backend", "gloo",
                            "--systems", "256"] + small, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
@@ -168,3 +174,9 @@ def test_four_ranks_line_is_the_driver_shape():
     keys = ("hist", "instructions", "rounds_total", "err_systems", "dropped", "digest_sum")
     for p4, p1 in zip(d4["sweep"]["points"], d1["sweep"]["points"]):
         assert {k: p4[k] for k in keys} == {k: p1[k] for k in keys}, (p4["cache_size"], p4["locality"])
+    # the line certifies itself: all four ranks held sampled ids in all 27 workloads, none differ
+    # from the oracle; no full-size slice golden covers 256 systems per rank (null, not false)
+    g = line["golden"]
+    assert g["samples"][0] >= 27 * 4 and g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == 4, g
+    assert g["headline"] is None and g["contention"] is None and g["sweep"] == [0, 0, 25]
+    assert all(r[line["sweep"]["cols"].index("smp_bad")] == 0 for r in line["sweep"]["rows"])

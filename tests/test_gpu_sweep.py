@@ -51,6 +51,7 @@ def test_sweep_grid_matches_oracle(gpus):
             assert p["cpu_baseline"]["kind"] == "reference", p["cpu_baseline_note"]
             assert f"CS={p['cache_size']}" in p["cpu_baseline"]["sample"]
             assert p["cpu_baseline"]["batches"]["n"] >= 3
+            assert f"locality {p['locality']:g}" in p["cpu_baseline"]["sample"]  # its own traces
             assert abs(p["vs_baseline"] - p["value"] / p["cpu_baseline"]["value"]) < 1e-9 * p["vs_baseline"]
 
 
@@ -83,7 +84,13 @@ def test_headline_line_carries_the_sweep():
             assert p[k] == want[k], (want["cache_size"], want["locality"], k)
         assert p["kernel_ms_avg"] <= p["ms_per_step"] and 0 < p["roofline"]["frac"] < 1
         assert p["cpu_baseline"]["kind"] == "reference", p["cpu_baseline_note"]
-        assert p["cpu_baseline"]["batches"]["n"] >= 3 and p["ub_frac"] == p["err_systems"] / GOLD["systems"]
+        assert p["cpu_baseline"]["batches"]["n"] >= 3 and p["err_frac"] == p["err_systems"] / GOLD["systems"]
+        # ub_frac counts only the reference's undefined sends (DASH_ERR_OOB / CTZ0)
+        assert p["ub_frac"] == p["ub_systems"] / GOLD["systems"] and p["ub_systems"] <= p["err_systems"]
+        # the reference on this point's own traces, every stalled instance explained or counted
+        assert f"locality {p['locality']:g}" in p["cpu_baseline"]["sample"]
+        st = p["cpu_baseline"]["stalled"]
+        assert st["n"] == p["cpu_baseline"]["hung_instances_killed"] and 0 <= st["explained"] <= st["n"]
     box = line["box"]
     assert box["device"]["compute_units"] > 0 and box["device"]["clock_khz"] > 0
     for k in ("probe_before", "probe_after"):

@@ -628,6 +628,14 @@ int dash_read_events(dash_t* h, uint64_t sys, dash_event* out, uint32_t cap, uin
         HIPCHK(h, hipMemcpyAsync(cnt.data(), h->d_event_count + sys * N, N * 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipMemcpyAsync(&sys_rounds, h->d_rounds + sys, 4, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
+        uint64_t total = 0, logged = 0;
+        for (uint32_t t = 0; t < N; t++) total += cnt[t];
+        // count-only call (out NULL, cap 0) on a log that holds every round the system ran: the
+        // per-node counts are the answer and nothing can be truncated, so skip the row copy
+        if (!out && sys_rounds <= R) {
+            *n = (uint32_t)std::min<uint64_t>(total, 0xFFFFFFFFull);
+            return DASH_OK;
+        }
         // only this run's rounds: the kernel writes the log up to its wave's last trip and never
         // clears it, so rows past the system's last active round may hold an earlier run's words
         // (ADVICE r4). Events only happen in rounds < rounds[sys]; copy whole 4-round rows of those.
@@ -641,8 +649,6 @@ int dash_read_events(dash_t* h, uint64_t sys, dash_event* out, uint32_t cap, uin
         }
         // the log is round-major (a node logs at most one event per round): reading it round by
         // round, node by node, is the lockstep order
-        uint64_t total = 0, logged = 0;
-        for (uint32_t t = 0; t < N; t++) total += cnt[t];
         uint32_t k = 0;
         for (uint32_t r = 0; r < std::min(Rs, sys_rounds); r++)
             for (uint32_t t = 0; t < N; t++) {

@@ -917,7 +917,7 @@ def golden_record(slice_ok, cont, points, totals, world, M):
     contention, and how many of the sweep points that have one are bit-exact: [equal, with a golden,
     points]), and the sampled ids summed over every workload of the run: [checked, mismatched, the
     fewest ranks holding samples in any workload, world]."""
-    objs = [samples_obj(totals, world)] + ([cont["totals"]["samples"]] if cont else []) + \
+    objs = [samples_obj(totals, world)] + ([cont["samples"]] if cont else []) + \
         [p["samples"] for p in points or []]
     flags = [p["golden_slice"] for p in points] if points else None
     return {"slice": [0, M], "headline": slice_ok, "contention": cont.get("golden_slice") if cont else None,
@@ -931,10 +931,12 @@ def golden_record(slice_ok, cont, points, totals, world, M):
                      "error bits"}
 
 
-def totals_dict(totals, world=1):
+def totals_dict(totals):
+    """The all-reduced totals (the same for any GPU count; the sampled-id check, whose rank count is
+    not, sits beside them as `samples`)."""
     return {"hist": totals[:13], "instructions_per_step": totals[13], "rounds_total": totals[14],
             "err_systems": totals[15], "dropped": totals[16], "digest_sum": totals[17:19],
-            "ub_systems": totals[19], "samples": samples_obj(totals, world)}
+            "ub_systems": totals[19]}
 
 
 def rank_spread(x, device):
@@ -1263,7 +1265,7 @@ def main():
                 "roofline": roofline(M, args.len, c_avg, c_prof, c_note),
                 "valu_issue": valu_issue(c_prof, c_stats["wave_rounds"]),
                 "tier_systems": c_stats["tier_systems"], "wave_rounds": c_stats["wave_rounds"],
-                "totals": totals_dict(c_tot, world), "golden_slice": c_slice_ok}
+                "totals": totals_dict(c_tot), "samples": samples_obj(c_tot, world), "golden_slice": c_slice_ok}
 
     # configs[4] beside the headline: the whole CACHE_SIZE x locality grid at
     # this line's systems per GPU, --line-sweep-warmup untimed and --line-sweep-steps timed steps per
@@ -1362,7 +1364,8 @@ def main():
             "wave_rounds": stats["wave_rounds"],
             # systems whose run hit the reference's undefined send to node 15 (ref :772,786):
             # parity there is with the engine's defined drop-and-flag rule
-            "totals": totals_dict(totals, world),
+            "totals": totals_dict(totals),
+            "samples": samples_obj(totals, world),
             "ub_frac": totals[19] / (world * M),
             "err_frac": totals[15] / (world * M),
             # the line certifies its own results at any GPU count -- rank 0's

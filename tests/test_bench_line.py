@@ -53,8 +53,7 @@ def synthetic_detail(world=8, with_all=True):
     smp = {"checked": 48 * world, "mismatched": 0, "ranks": world, "world": world}
     tot = {"hist": [15438985135] * 13, "instructions_per_step": 34359738368 * world,
            "rounds_total": 23801163240 * world, "err_systems": 51391 * world, "dropped": 60000 * world,
-           "digest_sum": [2251634405826991 * world, 2249834063518710 * world], "ub_systems": 51391 * world,
-           "samples": smp}
+           "digest_sum": [2251634405826991 * world, 2249834063518710 * world], "ub_systems": 51391 * world}
     probe = {"probe_ms": 163.759, "probe_valu_per_s": 839274538336.1628, "sclk_mhz": 1976.6,
              "sclk_min_mhz": 1853.2, "sclk_max_mhz": 2100.9, "sysfs": {"pci": "0000:dc:00.0", "power_w": 937.0}}
     return {
@@ -77,14 +76,14 @@ def synthetic_detail(world=8, with_all=True):
         "tier_systems": [M, 3, 0], "wave_rounds": 3018808080, "totals": tot, "ub_frac": 0.0490102767944336,
         "parity_note": "p" * 300,
         "contention": {"value": 6.78123456789e10 * world, "ms_per_step": 503.123456789, "roofline": _roof(),
-                       "totals": tot, "kernel_ms_avg": 503.0, "golden_slice": True},
+                       "totals": tot, "samples": smp, "kernel_ms_avg": 503.0, "golden_slice": True},
         "sweep": {"steps": 1, "warmup": 1, "cpu_per_cache_size": per_cs,
                   "golden": bench.sweep_golden_summary(pts, M), "points": pts},
         "next": {"events": {"slowdown": 1.10987654, "parity_same_digests_as_fast": True,
                             "parity_events_logged": True},
                  "seeded": {"slowdown": 1.48123456, "parity_all_issued": True, "parity_reproducible": True}},
         "box": {"probe_before": probe, "probe_after": probe, "device": {"name": "AMD Instinct MI355X"}},
-    } | {"golden": bench.golden_record(True, {"totals": tot, "golden_slice": True}, pts,
+    } | {"samples": smp, "golden": bench.golden_record(True, {"samples": smp, "golden_slice": True}, pts,
                                        tot["hist"] + [0] * 6 + [51391 * world, 48 * world, 0, world], world, M)}
 
 

@@ -122,7 +122,7 @@ def test_golden_record_summarises_every_workload():
     pts = [{"golden_slice": True, "samples": {"checked": 3, "mismatched": 0, "ranks": 8, "world": 8}}] * 24 + \
           [{"golden_slice": None, "samples": {"checked": 3, "mismatched": 1, "ranks": 7, "world": 8}}]
     tot = [0] * 20 + [5, 0, 8]
-    cont = {"totals": {"samples": {"checked": 5, "mismatched": 0, "ranks": 8, "world": 8}}, "golden_slice": True}
+    cont = {"samples": {"checked": 5, "mismatched": 0, "ranks": 8, "world": 8}, "golden_slice": True}
     g = bench.golden_record(True, cont, pts, tot, 8, 1 << 20)
     assert g["headline"] is True and g["contention"] is True and g["sweep"] == [24, 24, 25]
     assert g["samples"] == [5 + 5 + 75, 1, 7, 8]

@@ -61,7 +61,7 @@ def test_two_ranks_match_one_process():
     # both ranks checked their own sampled ids against the oracle's per-system results
     g = d2["_line"]["golden"]
     assert g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == 2 and g["samples"][0] > 0, g
-    assert d2["totals"]["samples"]["checked"] == d1["totals"]["samples"]["checked"] > 0
+    assert d2["samples"]["checked"] == d1["samples"]["checked"] > 0 and d2["samples"]["ranks"] == 2
     # value = all ranks' instructions / max-over-ranks time
     assert abs(d2["value"] - 4096 * 8 * 4096 / (d2["ms_per_step"] / 1e3)) < 1e-6 * d2["value"]
 

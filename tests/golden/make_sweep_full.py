@@ -1,12 +1,13 @@
 """Full-size golden totals for points of BASELINE.json configs[4] (the CACHE_SIZE x
-locality sweep; most of its 25 points are committed, the file lists them): the oracle (oracle/dash_oracle.c, test infrastructure) run over ALL 2^20
+locality sweep; all 25 points are committed since round 6, the file lists them): the oracle (oracle/dash_oracle.c, test infrastructure) run over ALL 2^20
 systems x 8 nodes x 4096 instructions of the locality generator, seed 0x5EED, at
   CACHE_SIZE 1, locality 0.0;  CACHE_SIZE 4, locality 0.5;  CACHE_SIZE 16, locality 1.0
 (the corners and the middle of the grid; round 4) and, since round 5, CACHE_SIZE 8, locality 0.0
 and CACHE_SIZE 16, locality 0.25 (the kernels round 5 changed: the 2-instruction trace window at
 CACHE_SIZE 8, the INV fan-out everywhere; 16 / 0.25 has the most REPLY_ID fan-outs and the most
 systems on the reference's undefined paths); later in round 5 more points one at a time
-(`make_sweep_full.py 8 CS:P ...`). Writes tests/golden/sweep_full.json: per point the
+(`make_sweep_full.py 8 CS:P ...`); round 6 the last two, CACHE_SIZE 2 and 16 at locality 0 (about
+30 min each on 7 threads). Writes tests/golden/sweep_full.json: per point the
 per-type histogram, instruction / round / error-system totals and bench.digest_sum of the
 per-system digests, so the `sweep` object of the default bench.py line (1M systems per GPU
 per point) is checked bit-exactly against the oracle: tests/test_full_size_golden.py

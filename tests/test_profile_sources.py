@@ -54,7 +54,15 @@ def _resolves(path):
             f = ROOT / b
             _bundles[b] = json.loads(f.read_text())["files"] if f.exists() else None
         return _bundles[b] is not None and any(k.startswith(prefix) for k in _bundles[b])
-    return (ROOT / path).exists()
+    if (ROOT / path).exists():
+        return True
+    # a record written before its source directory was bundled cites the directory's old path
+    parts = path.rstrip("/").split("/")
+    for i in range(len(parts) - 1, 1, -1):
+        b = "/".join(parts[:i]) + ".bundle.json"
+        if (ROOT / b).exists():
+            return _resolves(b + "#" + "/".join(parts[i:]))
+    return False
 
 
 def test_summaries_cite_sources():

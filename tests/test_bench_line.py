@@ -183,3 +183,32 @@ def test_committed_line_has_every_row_measured():
     assert all(v[0] >= 3 for v in sw["cpu"].values())
     assert len(sw["golden_bit_exact"]) >= 3 and all(sw["golden_bit_exact"])
     assert line["roofline"]["traffic"] and line["issue"]["waves_per_cu"] > 17
+
+
+@pytest.mark.parametrize("path,world", [("profiles/r06/ev6_a/bench.json", 1),
+                                        ("profiles/r06/two_rank_full/bench.json", 2)])
+def test_committed_r06_lines_certify_themselves(path, world):
+    """VERDICT r5 next #1 / #3 on the committed round-6 lines (the driver's command on one GPU, and
+    the same at N = 2 with both ranks on the box's GPU): rank 0's slice equals the full-size goldens
+    for the headline, contention and all 25 sweep points, every rank checked its sampled ids with no
+    mismatch, every stalled reference instance has a cause, and the line fits the driver's budget."""
+    f = ROOT / path
+    if not f.exists():
+        pytest.skip(f"{path} not committed yet")
+    text = [x for x in f.read_text().splitlines() if x.startswith("{")][-1]
+    assert len(text) <= bench.LINE_BUDGET
+    line = json.loads(text)
+    assert line["n_gpus"] == world
+    g = line["golden"]
+    assert g["slice"] == [0, 1 << 20] and g["headline"] is True and g["contention"] is True
+    assert g["sweep"] == [25, 25, 25]
+    checked, bad, ranks, w = g["samples"]
+    assert checked > 0 and bad == 0 and ranks == w == world
+    cols = line["sweep"]["cols"]
+    for row in line["sweep"]["rows"]:
+        r = dict(zip(cols, row))
+        assert r["golden"] is True and r["smp_bad"] == 0 and r["vs_baseline"] > 0, row
+    for cs, (points, batches, hung, explained) in line["sweep"]["cpu"].items():
+        assert points == 5 and batches >= 15 and explained == hung, cs
+    assert line["cpu_baseline"]["hung_explained"] == line["cpu_baseline"]["hung"]
+    assert line["ub_frac"] == pytest.approx(GOLD["uniform"]["err_systems"] / GOLD["systems"], rel=1e-2)

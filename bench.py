@@ -641,7 +641,7 @@ def sweep(args, dash, rank, world, dev):
                                          f"instr, CACHE_SIZE x locality grid (BASELINE configs[4])",
                              "parallelism": f"systems sharded over {world} GPU(s)"},
                   "vs_baseline_basis": SWEEP_CPU_BASIS,
-                  "sweep": {"steps": args.steps, "warmup": args.warmup, "cpu_per_cache_size": per_cs,
+                  "sweep": {"steps": args.steps, "warmup": args.warmup, "cpu_per_cache_size": per_cs, "notes": SWEEP_NOTES,
                             "golden": sweep_golden_summary(points, M), "points": points}}
 
         def compact(d, shown):
@@ -953,6 +953,8 @@ def rank_spread(x, device):
     return [float(lo.item()), float(hi.item())]
 
 
+# the CACHE_SIZE 8 trade, stated in the line rather than re-measured
+SWEEP_NOTES = {"8": "2-instr window: 18 not 16 waves/CU, p0 668->655 ms; L2 fills 8.5x algorithmic (CS4 5.1x), <1 TB/s"}
 SWEEP_CPU_BASIS = ("per point: the reference built for its CACHE_SIZE, mode (A), >= 3 batches on systems 0.. of "
                    "that point's own locality traces; each point's vs_baseline is against its own figure")
 
@@ -1060,7 +1062,7 @@ def compact_sweep(sw):
     return {"cols": ["cs", "p", "value_G", "ms_per_step", "frac", "vs_baseline", "ub_frac", "traffic_GB",
                      "golden", "smp_bad"],
             "rows": rows, "steps": sw["steps"],
-            "cpu_cols": ["points", "batches", "hung", "hung_explained"], "cpu": cpu}
+            "cpu_cols": ["points", "batches", "hung", "hung_explained"], "cpu": cpu, "notes": sw.get("notes")}
 
 
 def detail_path_arg(p):
@@ -1301,6 +1303,7 @@ def main():
                                      f"(BASELINE configs[4]; seed 0x{args.seed:X}, keyed by global id)",
                          "steps": args.line_sweep_steps, "warmup": args.line_sweep_warmup,
                          "cpu_baseline_basis": SWEEP_CPU_BASIS, "cpu_per_cache_size": sweep_cpu_obj,
+                         "notes": SWEEP_NOTES,
                          "golden": sweep_golden_summary(points, M), "points": points}
         cpu, cpu_b, port, note = None, None, None, None
         if not args.no_cpu_baseline:

@@ -77,7 +77,7 @@ def synthetic_detail(world=8, with_all=True):
         "parity_note": "p" * 300,
         "contention": {"value": 6.78123456789e10 * world, "ms_per_step": 503.123456789, "roofline": _roof(),
                        "totals": tot, "samples": smp, "kernel_ms_avg": 503.0, "golden_slice": True},
-        "sweep": {"steps": 1, "warmup": 1, "cpu_per_cache_size": per_cs,
+        "sweep": {"steps": 1, "warmup": 1, "cpu_per_cache_size": per_cs, "notes": bench.SWEEP_NOTES,
                   "golden": bench.sweep_golden_summary(pts, M), "points": pts},
         "next": {"events": {"slowdown": 1.10987654, "parity_same_digests_as_fast": True,
                             "parity_events_logged": True},
@@ -114,6 +114,7 @@ def test_worst_case_line_fits_the_budget(world, tmp_path, capsys):
                for r in line["sweep"]["rows"])
     assert all(v[1] >= 15 and v[3] == v[2] for v in line["sweep"]["cpu"].values())
     assert line["cpu_baseline"]["hung_explained"] == line["cpu_baseline"]["hung"]
+    assert "8.5x" in line["sweep"]["notes"]["8"]
     # the side file holds the full record
     assert json.loads((long_dir / "bench_detail.json").read_text()) == json.loads(json.dumps(d))
 

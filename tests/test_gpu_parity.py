@@ -616,7 +616,7 @@ def test_engine_reenacts_reference_runs(dash, n):
     assert k == 40
 
 
-def reenact_micro(dash, n, name):
+def reenact_micro(dash, n, name, want_err=0):
     import ref_pin
     k = 0
     for c, cs, tr, lens, acts, _ in ref_pin.micro_cases(n, name):
@@ -627,6 +627,7 @@ def reenact_micro(dash, n, name):
             dig = int(eng.read_results()[0][0])
             ev = eng.read_events(0)
         assert not st["err_bits"] & (dash.ERR_ROUNDCAP | dash.ERR_DEADLOCK), c["seed"]  # ran to quiescence
+        assert st["err_bits"] & want_err == want_err, c["seed"]
         assert dig == int(c["digest"], 16), c["seed"]
         got = ref_pin.event_tokens([(e.node, e.kind == dash.EV_INSTR, e.word) for e in ev], n)
         assert got == c["log"], c["seed"]
@@ -652,6 +653,18 @@ def test_engine_reenacts_non_round_model_runs(dash, n):
     are delivered one per round), the engine's event log equals the reference's DEBUG_MSG /
     DEBUG_INSTR lines thread by thread, and its final state is the reference's dumps (digest)."""
     assert reenact_micro(dash, n, "micro") == 40
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_engine_reenacts_reference_runs_through_the_undefined_send(dash, n):
+    """The reference's undefined send pinned on the reference itself: 40 runs
+    per node count of the reference pin binary that evicted a never-filled 0xFF line to node 15
+    (assignment.c:772,786; its own stderr shows the receiver guard dropping it,
+    tests/golden/ref_runs/ub{n}.json, make_ref_ub.py), re-enacted through the interleaving the
+    oracle recovered from their logs: the engine drops and flags the same send (DASH_ERR_OOB), its
+    event log equals the reference's thread by thread and its final state is the reference's
+    dumps."""
+    assert reenact_micro(dash, n, "ub", want_err=dash.ERR_OOB) == 40
 
 
 @pytest.mark.parametrize("N,CS", [(2, 1), (3, 3), (4, 4), (5, 16), (8, 2), (8, 4)])

@@ -34,3 +34,13 @@ def test_ub_runs_replay_to_the_reference_dumps(n):
         k += 1
     assert k == len(data["cases"]) == 40
     assert {c["cache_size"] for c in data["cases"]} == {1, 4}
+
+
+@pytest.mark.parametrize("n,cs,kind,loc", [(8, 4, 0, 0), (8, 16, 2, 0), (4, 1, 1, 0), (8, 2, 2, 49152)])
+def test_ctz0_path_is_unreachable(n, cs, kind, loc):
+    """an EM directory entry always holds exactly one sharer bit, so the reference's
+    __builtin_ctz(0) (ref :209,451) cannot happen and DASH_ERR_CTZ0 is a defensive flag. The oracle
+    over 20,000 random systems per configuration never raises it (while OOB does occur)."""
+    r = oc.run_batch(0xC720, 0, 20000, num_procs=n, cache_size=cs, length=64, kind=kind,
+                     locality=loc, threads=4)
+    assert not (r["errors"] & oc.ERR_CTZ0).any()

@@ -23,4 +23,10 @@ if [ -z "${SKIP_TRACE:-}" ]; then
       python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --contention-steps 0 --line-sweep off --line-next off \
       --detail "$OUT/trace_uniform_detail.json" > "$OUT/trace_uniform.log" 2>&1 || exit 1
 fi
+if [ -n "${DEFAULT_STATS:-}" ]; then
+  step "rocprofv3 --kernel-trace --stats of the whole default command"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/default_cmd_stats" -o run -- \
+      python3 bench.py --gpus 1 --steps 20 --warmup 5 --detail "$OUT/default_cmd_stats_detail.json" \
+      > "$OUT/default_cmd_stats.json" 2> "$OUT/default_cmd_stats.err" || exit 1
+fi
 step evidence-done

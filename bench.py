@@ -122,18 +122,35 @@ def ref_exe(cache_size):
 
 
 WRITEBACK_INV, WRITEBACK_INT = 7, 8  # message types whose receiver comes from __builtin_ctz (ref :209,451)
+# causes that name the reference rule behind the stall; the others only describe its state
 STALL_EXPLAINED = ("ctz0_send", "queue_full")
+MSG_BUFFER_SIZE = 256  # ref :9
+
+
+def snapshots(stderr_text):
+    """The instance's SIGUSR1 snapshot lines (oracle/patch_ref.py patch 6), parsed: [{"done",
+    "inflight", "queues": [(head, tail, count)] * NUM_PROCS}]."""
+    out = []
+    for ln in stderr_text.splitlines():
+        if not ln.startswith("bench: snapshot "):
+            continue
+        f = ln.split()
+        qs = [tuple(int(x) for x in tok.split(":")[1].split(",")) for tok in f[6:]]
+        out.append({"done": int(f[3]), "inflight": int(f[5]), "queues": qs})
+    return out
 
 
 def stall_cause(stderr_text, num_procs=8):
-    """Why a killed reference instance stalled, from its own stderr (oracle/patch_ref.py patch 5):
-    "ctz0_send" = it dropped a WRITEBACK_INT / WRITEBACK_INV addressed to a node >= NUM_PROCS other
-    than 15 -- the reference's __builtin_ctz(0) (tzcnt gives 32; ref :209,451), after which that
-    request's requester waits forever; "queue_full" = a full queue dropped a message (ref :758-762;
-    at 256 the consumer's head != tail test also stops draining, ref :167-170); "oob_evict_only" =
-    only the 0xFF-line evictions to node 15 were dropped (ref :772,786; nobody waits on those);
-    "none_logged" = no drop at all."""
-    cause = "none_logged"
+    """Why a killed reference instance stalled, from its own stderr (oracle/patch_ref.py patches 5
+    and 6). From its drop notes: "ctz0_send" = it dropped a WRITEBACK_INT / WRITEBACK_INV addressed
+    to a node >= NUM_PROCS other than 15 -- the reference's __builtin_ctz(0) (tzcnt gives 32; ref
+    :209,451), whose requester then waits forever; "queue_full" = a full queue dropped a message (ref
+    :758-762; at 256 the drain loop's head != tail test never pops it again, ref :167-170). Else from
+    its last snapshot (taken after a second without any queue moving): a queue at 256 is
+    "queue_full"; every queue empty and nothing in flight while a thread is not done is
+    "waits_with_nothing_in_flight" (a node waits for a reply no one will send); otherwise
+    "stuck_with_messages" (and "no_snapshot" without one)."""
+    cause = None
     for ln in stderr_text.splitlines():
         f = ln.split()
         if ln.startswith("bench: queue full"):
@@ -142,9 +159,38 @@ def stall_cause(stderr_text, num_procs=8):
             t, r = int(f[2]), int(f[5])
             if t in (WRITEBACK_INV, WRITEBACK_INT) and r >= num_procs and r != 15:
                 cause = "ctz0_send"
-            elif cause == "none_logged":
-                cause = "oob_evict_only"
-    return cause
+    if cause:
+        return cause
+    snap = snapshots(stderr_text)
+    if not snap:
+        return "no_snapshot"
+    last = snap[-1]
+    if any(c >= MSG_BUFFER_SIZE for _, _, c in last["queues"]):
+        return "queue_full"
+    if last["inflight"] == 0 and all(c == 0 for _, _, c in last["queues"]) and last["done"] < num_procs:
+        return "waits_with_nothing_in_flight"
+    return "stuck_with_messages"
+
+
+def still_moving(stderr_text):
+    """True when the instance's last two snapshots differ (a queue moved between them)."""
+    snap = snapshots(stderr_text)
+    return len(snap) >= 2 and snap[-1] != snap[-2]
+
+
+def probe_late(procs, late, dirs, gap=1.0):
+    """Two SIGUSR1 snapshots `gap` s apart of each still-running instance in `late`; returns the
+    ones whose queues moved in between (slow, not stalled)."""
+    import signal
+    for i in late:
+        if procs[i].poll() is None:
+            procs[i].send_signal(signal.SIGUSR1)
+    time.sleep(gap)
+    for i in late:
+        if procs[i].poll() is None:
+            procs[i].send_signal(signal.SIGUSR1)
+    time.sleep(0.2)
+    return [i for i in late if procs[i].poll() is None and still_moving((dirs[i] / "stderr.txt").read_text())]
 
 
 def explain_stalls(stalls, seed, kind_id, locality, cache_size, length):
@@ -165,8 +211,9 @@ def explain_stalls(stalls, seed, kind_id, locality, cache_size, length):
             # system id -> [times it stalled, the oracle's error bits for it under lockstep]
             "systems": {str(i): [n, flags[i]] for i, n in sorted(by_sys.items())},
             "oracle_ctz0": sum(n for i, n in by_sys.items() if flags[i] & ERR_CTZ0),
-            "basis": "cause from the instance's own stderr (oracle/patch_ref.py patch 5); the oracle runs the "
-                     "same system under the engine's lockstep schedule"}
+            "basis": "killed only after two SIGUSR1 snapshots a second apart showed no queue moving; cause from "
+                     "the instance's own stderr (oracle/patch_ref.py patches 5, 6: drop notes, last snapshot); the "
+                     "oracle runs the same system under the engine's lockstep schedule"}
 
 
 def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, locality=0, kind_name=None,
@@ -201,12 +248,14 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
                     lines.append(f"WR {a:02X} {v}\n" if w & 0x8000 else f"RD {a:02X}\n")
                 (d / "tests" / "b" / f"core_{n}.txt").write_text("".join(lines))
             dirs.append(d)
-        # The reference can stall for good under some thread schedules (e.g. its undefined
-        # __builtin_ctz(0), ref :209,451, sends to "node 32", which the patch drops, and the
-        # requester then waits forever). An instance still running well after the batch's others
-        # finished (4x the slowest finisher, at least 5 s; or --ref-timeout) is killed and not
-        # counted: instructions and time are those of the instances that finished.
+        # The reference can stall for good under some thread schedules (a queue that reaches 256 is
+        # never drained again, ref :167-170). An instance still running well after the batch's
+        # others finished (4x the slowest finisher, at least 5 s) is probed: two SIGUSR1 snapshots a
+        # second apart (patch 6). If a queue moved it is slow, not stalled, and the batch waits on
+        # (until --ref-timeout); if nothing moved it is killed and not counted -- instructions and
+        # time are those of the instances that finished -- and its cause is read from its stderr.
         batches, hung, instr, elapsed, t0 = 0, 0, 0, 0.0, time.perf_counter()
+        waited_slow = 0  # late instances found still moving and waited for
         rates = []  # per batch: finished instances' instructions / the batch's slowest finisher
         stalls = []  # per killed instance: (system id, cause from its own stderr)
         while True:
@@ -215,6 +264,7 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
                      for d, f in zip(dirs, errs)]
             tb = last = time.perf_counter()
             fin = {}
+            extend, slow_seen = 0.0, set()
             try:
                 while len(fin) < k:
                     time.sleep(0.005)
@@ -225,7 +275,15 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
                                 raise RuntimeError(f"reference instance exited with {p.returncode}")
                             fin[i] = now - tb
                     limit = max(5.0, 4 * max(fin.values())) if fin else args.ref_timeout
+                    limit = max(limit, extend)
                     if len(fin) < k and now - tb > min(limit, args.ref_timeout):
+                        late = [i for i in range(k) if i not in fin]
+                        moving = probe_late(procs, late, dirs) if now - tb < args.ref_timeout else []
+                        if moving:  # slow, not stalled: wait another `limit` seconds and look again
+                            waited_slow += len(set(moving) - slow_seen)
+                            slow_seen |= set(moving)
+                            extend = time.perf_counter() - tb + max(5.0, 4 * max(fin.values()) if fin else 5.0)
+                            continue
                         hung += sum(1 for i in range(k) if i not in fin)
                         break
                     if now - last > 30:
@@ -254,7 +312,7 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
     loc = f", locality {locality / 65536:g}" if kind_name == "locality" else ""
     stalled = explain_stalls(stalls, seed, kind_id, locality, cache_size, args.len)
     return {"value": instr / elapsed, "unit": "instr/s", "cores": cores, "host_cpus_visible": host_cpus_visible(),
-            "stalled": stalled,
+            "stalled": stalled, "slow_instances_waited_for": waited_slow,
             "kind": "reference", "mode": "A" if k == cores else ("B" if k == 1 else f"{k} instances"),
             # spread over the batches (the spinning instances vary from batch to batch): instr/s
             "batches": {"n": len(rates), "min": min(rates), "median": sorted(rates)[len(rates) // 2],

@@ -25,6 +25,12 @@ The patch (each edit is anchored on text that must occur exactly once):
      <type>`, so bench.py can say why an instance it killed had stalled (a WRITEBACK_INT /
      WRITEBACK_INV sent to node 32 is the reference's __builtin_ctz(0), ref :209,451: its requester
      then waits forever). Only the drop paths print; the handlers are untouched.
+  6. (round 6) SIGUSR1 prints one snapshot line on stderr -- `bench: snapshot done <threads done>
+     inflight <messages in flight> q<n>:<head>,<tail>,<count> ...` for every queue -- from an
+     async-signal-safe handler reading the globals (ref :102 and patch 4's counters). bench.py
+     sends it twice, a second apart, to an instance that outlives the batch: unchanged snapshots
+     mean no message moved (stalled, killed); changed ones mean a slow instance, which is waited
+     for. Nothing on the simulation path changes.
 Everything else -- the handlers, locks, spinning, state dumps -- is the reference.
 """
 import pathlib
@@ -46,6 +52,30 @@ EDITS = [
      "    if ( __atomic_fetch_or( &bench_noted, bit, __ATOMIC_SEQ_CST ) & bit ) return;\n"
      "    if ( full ) fprintf( stderr, \"bench: queue full at node %d, dropped %d\\n\", receiver, type );\n"
      "    else fprintf( stderr, \"bench: dropped %d to node %d\\n\", type, receiver );\n"
+     "}\n"
+     "#include <signal.h>\n"
+     "#include <unistd.h>\n"
+     "static void bench_put( char **p, const char *s, long v ) {  /* patch 6 */\n"
+     "    char t[24]; int n = 0;\n"
+     "    while ( *s ) *( *p )++ = *s++;\n"
+     "    if ( v < 0 ) { *( *p )++ = '-'; v = -v; }\n"
+     "    do { t[ n++ ] = (char)( '0' + v % 10 ); v /= 10; } while ( v );\n"
+     "    while ( n ) *( *p )++ = t[ --n ];\n"
+     "}\n"
+     "static void bench_snapshot( int sig ) {\n"
+     "    char buf[ 64 + 48 * NUM_PROCS ], *p = buf;\n"
+     "    (void)sig;\n"
+     "    bench_put( &p, \"bench: snapshot done \", __atomic_load_n( &bench_done, __ATOMIC_SEQ_CST ) );\n"
+     "    bench_put( &p, \" inflight \", __atomic_load_n( &bench_inflight, __ATOMIC_SEQ_CST ) );\n"
+     "    for ( int i = 0; i < NUM_PROCS; i++ ) {\n"
+     "        bench_put( &p, \" q\", i );\n"
+     "        bench_put( &p, \":\", messageBuffers[ i ].head );\n"
+     "        bench_put( &p, \",\", messageBuffers[ i ].tail );\n"
+     "        bench_put( &p, \",\", __atomic_load_n( &messageBuffers[ i ].count, __ATOMIC_SEQ_CST ) );\n"
+     "    }\n"
+     "    *p++ = '\\n';\n"
+     "    ssize_t w = write( 2, buf, (size_t)( p - buf ) );\n"
+     "    (void)w;\n"
      "}\n"),
     ("                messageBuffers[ threadId ].count > 0 &&",
      "                __atomic_load_n( &messageBuffers[ threadId ].count, __ATOMIC_SEQ_CST ) > 0 &&"),
@@ -78,6 +108,8 @@ EDITS = [
     ("      buf->count++;\n",
      "      __atomic_fetch_add( &bench_inflight, 1, __ATOMIC_SEQ_CST );\n"
      "      __atomic_fetch_add( &buf->count, 1, __ATOMIC_SEQ_CST );\n"),
+    ("    omp_set_num_threads(NUM_PROCS);\n",
+     "    omp_set_num_threads(NUM_PROCS);\n    signal( SIGUSR1, bench_snapshot );  /* patch 6 */\n"),
     ("    } else {\n#ifdef DEBUG\n        fprintf(stderr, \"Error: Message buffer overflow",
      "    } else {\n        bench_note_drop( receiver, msg.type, 1 );  /* patch 5 */\n"
      "#ifdef DEBUG\n        fprintf(stderr, \"Error: Message buffer overflow"),

@@ -129,11 +129,24 @@ def test_golden_record_summarises_every_workload():
 
 
 def test_stall_cause_reads_the_patch_notes():
-    assert bench.stall_cause("") == "none_logged"
-    assert bench.stall_cause("bench: dropped 11 to node 15\n") == "oob_evict_only"
+    assert bench.stall_cause("") == "no_snapshot"
     assert bench.stall_cause("bench: dropped 12 to node 15\nbench: dropped 8 to node 32\n") == "ctz0_send"
     assert bench.stall_cause("bench: dropped 7 to node 32\n") == "ctz0_send"
     assert bench.stall_cause("bench: queue full at node 0, dropped 9\n") == "queue_full"
+
+
+SNAP = "bench: snapshot done {d} inflight {f} q0:{q0} q1:{q1}\n"
+
+
+def test_stall_cause_reads_the_snapshots():
+    """patch 6: the last SIGUSR1 snapshot says what a stalled instance was doing (2 nodes here)."""
+    idle = SNAP.format(d=1, f=0, q0="5,5,0", q1="9,9,0")
+    assert bench.stall_cause("bench: dropped 11 to node 15\n" + idle * 2, 2) == "waits_with_nothing_in_flight"
+    assert bench.stall_cause(SNAP.format(d=1, f=256, q0="7,7,256", q1="1,1,0") * 2, 2) == "queue_full"
+    assert bench.stall_cause(SNAP.format(d=0, f=3, q0="1,3,2", q1="4,5,1") * 2, 2) == "stuck_with_messages"
+    assert not bench.still_moving(idle * 2) and not bench.still_moving(idle)
+    assert bench.still_moving(idle + SNAP.format(d=1, f=1, q0="5,6,1", q1="9,9,0"))
+    assert bench.snapshots(idle)[0] == {"done": 1, "inflight": 0, "queues": [(5, 5, 0), (9, 9, 0)]}
 
 
 def test_patch_ref_has_the_drop_notes():
@@ -142,3 +155,31 @@ def test_patch_ref_has_the_drop_notes():
     src = (ROOT / "oracle" / "patch_ref.py").read_text()
     assert "bench_note_drop( receiver, msg.type, 0 )" in src and "bench_note_drop( receiver, msg.type, 1 )" in src
     assert 'bench: dropped %d to node %d' in src and 'bench: queue full at node %d, dropped %d' in src
+    assert "signal( SIGUSR1, bench_snapshot )" in src and "bench: snapshot done " in src
+
+
+def test_probe_sees_a_running_reference_move(tmp_path):
+    """patch 6 end to end on the real benchmark binary: a reference instance probed while it runs
+    answers both SIGUSR1s with snapshots that differ, so bench.py would wait for it, not kill it."""
+    import subprocess
+    import time
+    exe = bench.ref_exe(4)
+    if not exe.exists():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    tr = oc.gen_system(0x5EED, 3, num_procs=8, length=4096, kind=0)
+    (tmp_path / "tests" / "b").mkdir(parents=True)
+    for n in range(8):
+        (tmp_path / "tests" / "b" / f"core_{n}.txt").write_text("".join(
+            f"WR {(w >> 8) & 0x7F:02X} {w & 0xFF}\n" if w & 0x8000 else f"RD {(w >> 8) & 0x7F:02X}\n"
+            for w in tr[n].tolist()))
+    with open(tmp_path / "stderr.txt", "w") as f:
+        p = subprocess.Popen([str(exe), "b"], cwd=tmp_path, stdout=subprocess.DEVNULL, stderr=f)
+        time.sleep(0.05)
+        moving = bench.probe_late([p], [0], [tmp_path], gap=0.1)
+        running = p.poll() is None
+        p.wait(timeout=120)
+    assert p.returncode == 0  # the handler returns; the run completes and dumps
+    snaps = bench.snapshots((tmp_path / "stderr.txt").read_text())
+    if not running or len(snaps) < 2:
+        pytest.skip("the instance finished before the second snapshot")
+    assert moving == [0] and len(snaps[0]["queues"]) == 8

@@ -181,3 +181,22 @@ def test_four_ranks_line_is_the_driver_shape():
     assert g["samples"][0] >= 27 * 4 and g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == 4, g
     assert g["headline"] is None and g["contention"] is None and g["sweep"] == [0, 0, 25]
     assert all(r[line["sweep"]["cols"].index("smp_bad")] == 0 for r in line["sweep"]["rows"])
+
+
+def test_eight_ranks_line_certifies_itself():
+    """The driver's N = 8 line shape, rehearsed with eight ranks on the box's one GPU over gloo (256
+    systems per rank, the golden fixtures' 4096 instructions, the sweep in the line): all eight ranks
+    hold sampled ids in all 27 workloads and none differs from the oracle; the line fits 4 KB."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    small = ["--len", "4096", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--contention-steps", "1",
+             "--line-sweep", "on", "--line-sweep-warmup", "0", "--systems", "256"]
+    eight = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "8", "--dist-backend", "gloo"] + small,
+                           capture_output=True, text=True, timeout=500, env=env, cwd=ROOT)
+    assert eight.returncode == 0, eight.stderr[-3000:]
+    d8 = _line(eight.stdout)
+    line = d8["_line"]
+    assert line["n_gpus"] == 8 and line["rccl_world"] == 8
+    g = line["golden"]
+    assert g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == 8, g
+    assert g["samples"][0] >= 27 * 8
+    assert d8["totals"]["instructions_per_step"] == 8 * 256 * 8 * 4096

@@ -845,3 +845,30 @@ def test_probe_box_reports_the_device(dash):
     assert b["probe_sclk_min_mhz"] <= b["probe_sclk_mhz"] <= b["probe_sclk_max_mhz"]
     with pytest.raises(dash.DashError):
         dash.probe_box(99)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_every_rank_slice_of_the_eight_gpu_layout(dash, kind):
+    """What each rank of the driver's 8-GPU run computes, on one GPU, one slice at a time: global
+    systems [r * 2^20, (r + 1) * 2^20) for r = 0..7 (bench.shard; traces keyed by global id), full
+    size, uniform / contention. Every slice's sampled systems (tests/golden/rank_samples.json, the
+    fixture the bench line checks at any N) equal the oracle's per-system digest, rounds and error
+    bits; slice 0's totals equal the full-size golden (the slice rank 0 certifies in every line)."""
+    import argparse
+    args = argparse.Namespace(len=4096, seed=0x5EED)
+    key = ("uniform", "contention")[kind]
+    M = 1 << 20
+    checked = 0
+    with dash.Engine(M, num_procs=8, cache_size=4, max_instr=4096) as eng:
+        for r in range(8):
+            eng.generate(0x5EED, 4096, kind=kind, sys_base=r * M)
+            st = eng.run()
+            d, rnd, e = eng.read_results()
+            c, bad = bench.sample_check(key, 4, r * M, M, args, d, rnd, e)
+            assert c >= 16 and bad == 0, (r, c, bad)
+            checked += c
+            if r == 0:
+                local = {"hist": st["hist"], "instructions": st["instructions"], "rounds_total": st["rounds_total"],
+                         "err_systems": st["err_systems"], "digest_sum": bench.digest_sum(d)}
+                assert bench.slice_golden(key, 4, local, 0, M, args) is True
+    assert checked == sum(1 for _ in json.loads((GOLDEN.parent / "rank_samples.json").read_text())["ids"])

@@ -121,6 +121,19 @@ def ref_exe(cache_size):
     return ROOT / "oracle" / "_ref" / name
 
 
+_TRACE_LINES = []
+
+
+def trace_lines():
+    """The reference's trace line (`RD XX` / `WR XX v`, ref :835-845) of every packed 16-bit record,
+    as bytes, indexed by the record (an RD's value bits are ignored): a table lookup per instruction
+    when bench.py writes the reference's input files (16-128 instances x 8 nodes x 4096 lines per leg)."""
+    if not _TRACE_LINES:
+        _TRACE_LINES.extend((f"WR {(w >> 8) & 0x7F:02X} {w & 0xFF}\n" if w & 0x8000 else
+                             f"RD {(w >> 8) & 0x7F:02X}\n").encode() for w in range(1 << 16))
+    return _TRACE_LINES
+
+
 WRITEBACK_INV, WRITEBACK_INT = 7, 8  # message types whose receiver comes from __builtin_ctz (ref :209,451)
 # causes that name the reference rule behind the stall; the others only describe its state
 STALL_EXPLAINED = ("ctz0_send", "queue_full")
@@ -242,11 +255,8 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
             (d / "tests" / "b").mkdir(parents=True)
             tr = oc.gen_system(seed, i, num_procs=8, length=args.len, kind=kind_id, locality=locality)
             for n in range(8):
-                lines = []
-                for w in tr[n].tolist():
-                    a, v = (w >> 8) & 0x7F, w & 0xFF
-                    lines.append(f"WR {a:02X} {v}\n" if w & 0x8000 else f"RD {a:02X}\n")
-                (d / "tests" / "b" / f"core_{n}.txt").write_text("".join(lines))
+                (d / "tests" / "b" / f"core_{n}.txt").write_bytes(b"".join(map(trace_lines().__getitem__,
+                                                                               tr[n].tolist())))
             dirs.append(d)
         # The reference can stall for good under some thread schedules (a queue that reaches 256 is
         # never drained again, ref :167-170). An instance still running well after the batch's

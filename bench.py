@@ -246,7 +246,9 @@ def ref_baseline(args, seed, kind_id, target_s, instances=0, cache_size=4, local
     if not exe.exists():
         raise RuntimeError(f"{exe.relative_to(ROOT)} missing (built by __graft_entry__.build() / "
                            f"oracle/build_ref.sh where /root/reference exists)")
-    k = instances or host_cores()
+    # mode (A) is one instance per host core, capped (--ref-max-instances): each instance spins 8
+    # threads, and a large node's quota would otherwise start thousands of them at once
+    k = instances or min(host_cores(), getattr(args, "ref_max_instances", 64))
     kind_name = kind_name or args.kind
     with tempfile.TemporaryDirectory() as td:
         dirs = []
@@ -1207,6 +1209,9 @@ def main():
     ap.add_argument("--ref-instances", type=int, default=0,
                     help="concurrent reference instances (0 = one per host core: BASELINE.md mode (A); "
                          "1 = mode (B))")
+    ap.add_argument("--ref-max-instances", type=int, default=64,
+                    help="cap on mode (A)'s concurrent instances (8 threads each); a capped run reports "
+                         "mode '<k> instances' instead of 'A'")
     ap.add_argument("--ref-timeout", type=float, default=240.0,
                     help="give up on the reference baseline after this many seconds (reported as null)")
     ap.add_argument("--first-depth", type=int, choices=[0, 32, 256], default=0,

@@ -162,7 +162,8 @@ def stall_cause(stderr_text, num_procs=8):
     its last snapshot (taken after a second without any queue moving): a queue at 256 is
     "queue_full"; every queue empty and nothing in flight while a thread is not done is
     "waits_with_nothing_in_flight" (a node waits for a reply no one will send); otherwise
-    "stuck_with_messages" (and "no_snapshot" without one)."""
+    "stuck_with_messages" (and "no_snapshot" without one; "still_moving_at_timeout" for a slow
+    instance killed only at --ref-timeout)."""
     cause = None
     for ln in stderr_text.splitlines():
         f = ln.split()
@@ -177,6 +178,8 @@ def stall_cause(stderr_text, num_procs=8):
     snap = snapshots(stderr_text)
     if not snap:
         return "no_snapshot"
+    if len(snap) >= 2 and snap[-1] != snap[-2]:
+        return "still_moving_at_timeout"  # slow, killed only at --ref-timeout
     last = snap[-1]
     if any(c >= MSG_BUFFER_SIZE for _, _, c in last["queues"]):
         return "queue_full"

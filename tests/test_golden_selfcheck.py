@@ -145,6 +145,8 @@ def test_stall_cause_reads_the_snapshots():
     assert bench.stall_cause(SNAP.format(d=1, f=256, q0="7,7,256", q1="1,1,0") * 2, 2) == "queue_full"
     assert bench.stall_cause(SNAP.format(d=0, f=3, q0="1,3,2", q1="4,5,1") * 2, 2) == "stuck_with_messages"
     assert not bench.still_moving(idle * 2) and not bench.still_moving(idle)
+    moved = idle + SNAP.format(d=1, f=1, q0="5,6,1", q1="9,9,0")
+    assert bench.stall_cause(moved, 2) == "still_moving_at_timeout"
     assert bench.still_moving(idle + SNAP.format(d=1, f=1, q0="5,6,1", q1="9,9,0"))
     assert bench.snapshots(idle)[0] == {"done": 1, "inflight": 0, "queues": [(5, 5, 0), (9, 9, 0)]}
 

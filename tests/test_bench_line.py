@@ -187,6 +187,7 @@ def test_committed_line_has_every_row_measured():
 
 
 @pytest.mark.parametrize("path,world", [("profiles/r06/ev6_a/bench.json", 1), ("profiles/r06/ev6_c/bench.json", 1),
+                                        ("profiles/r06/ev6_d/bench.json", 1),
                                         ("profiles/r06/two_rank_full/bench.json", 2)])
 def test_committed_r06_lines_certify_themselves(path, world):
     """VERDICT r5 next #1 / #3 on the committed round-6 lines (the driver's command on one GPU, and

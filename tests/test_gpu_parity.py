@@ -375,6 +375,28 @@ def test_micro_schedule_stepping_a_node_with_held_sends_is_flagged(dash):
     assert st["err_bits"] & dash.ERR_SCHEDULE
 
 
+def test_event_count_only_call(dash):
+    """dash_read_events(h, sys, NULL, 0, &n) counts without copying the log's rows when
+    the log holds every round the system ran -- the same count as a full read and as the oracle's
+    log -- and still reports DASH_ETRUNC (with the full count) when it does not."""
+    import ctypes
+    tr, lens = load_test_dir(GOLDEN / "test_4")
+    _, log = run_system(tr, lens, log=True, log_msgs=True)
+    lib = dash.lib()
+    n = ctypes.c_uint32()
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4096) as eng:
+        eng.load_traces(tr[None], lens[None])
+        eng.run()
+        assert lib.dash_read_events(eng.h, 0, None, 0, ctypes.byref(n)) == dash.OK
+        assert n.value == len(eng.read_events(0)) == len(log.splitlines())
+        total = n.value
+    with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4) as eng:
+        eng.load_traces(tr[None], lens[None])
+        eng.run()
+        assert lib.dash_read_events(eng.h, 0, None, 0, ctypes.byref(n)) == dash.ETRUNC
+        assert n.value == total
+
+
 def test_debug_trace_truncation_is_reported(dash):
     tr, lens = load_test_dir(GOLDEN / "test_4")
     with dash.Engine(1, num_procs=4, cache_size=4, max_instr=32, trace_events=4) as eng:

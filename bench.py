@@ -508,12 +508,21 @@ def golden_key(kind_name, cache_size, locality=None):
 
 
 def slice_golden(key, cache_size, local, sys_base, M, args):
-    """This rank's own (pre-reduce) totals against the oracle's full-size totals of global systems
-    [0, 2^20): tests/golden/full_size.json (uniform, contention) and sweep_full.json (configs[4]).
-    True / False when this rank owns exactly that slice and a golden exists for the workload, else
-    None. At any GPU count rank 0 owns [0, 2^20) (shard()), so every driver line is checked."""
-    if sys_base != 0:
+    """This rank's own (pre-reduce) totals against the oracle's full-size totals of its slice. Slice 0
+    = global systems [0, 2^20): tests/golden/full_size.json (uniform, contention) and sweep_full.json
+    (configs[4]); slices r = 1..7 of the 8-GPU layout, [r * 2^20, (r + 1) * 2^20):
+    tests/golden/full_slices.json (uniform, contention; make_full_slices.py). True / False when this
+    rank owns exactly such a slice and a golden exists for it, else None. At any GPU count rank 0
+    owns slice 0 (shard()), so every driver line is checked; at 2^20 systems per GPU every rank is."""
+    if M != 1 << 20 or sys_base % M:
         return None
+    r = sys_base // M
+    if r:
+        g = golden_file("full_slices.json")
+        gp = (g or {}).get(key, {}).get(str(r)) if g and g.get("cache_size") == cache_size else None
+        if not gp or (g["systems_per_slice"], g["instr_per_node"], g["seed"]) != (M, args.len, args.seed):
+            return None
+        return all(local[k] == gp[k] for k in ("hist", "instructions", "rounds_total", "err_systems", "digest_sum"))
     if key in ("uniform", "contention"):
         g = golden_file("full_size.json")
         gp = g.get(key) if g and g.get("cache_size") == cache_size else None
@@ -545,8 +554,9 @@ def sample_check(key, cache_size, sys_base, M, args, digests, rounds, errors):
 
 
 # the all-reduced counter vector of one workload: hist[13], instructions, rounds_total, err_systems,
-# dropped, digest_sum[2], ub_systems, sampled systems checked, sampled mismatches, ranks with samples
-N_COUNTERS = 23
+# dropped, digest_sum[2], ub_systems, sampled systems checked, sampled mismatches, ranks with samples,
+# ranks whose whole slice has a golden, ranks whose slice equals it
+N_COUNTERS = 25
 
 
 def local_totals(eng, stats, key, cache_size, sys_base, M, args):
@@ -558,15 +568,18 @@ def local_totals(eng, stats, key, cache_size, sys_base, M, args):
              "err_systems": stats["err_systems"], "digest_sum": dsum}
     ub = int(((e & (ERR_OOB | ERR_CTZ0)) != 0).sum())
     checked, bad = sample_check(key, cache_size, sys_base, M, args, d, r, e)
+    ok = slice_golden(key, cache_size, local, sys_base, M, args)
     vec = (stats["hist"] + [stats["instructions"], stats["rounds_total"], stats["err_systems"], stats["dropped"]]
-           + dsum + [ub, checked, bad, 1 if checked else 0])
-    return vec, slice_golden(key, cache_size, local, sys_base, M, args)
+           + dsum + [ub, checked, bad, 1 if checked else 0, 0 if ok is None else 1, 1 if ok else 0])
+    return vec, ok
 
 
 def samples_obj(totals, world):
     """The sampled-id check summed over the ranks: systems checked, mismatches, ranks that held
-    samples (all of them when the ranks' slices are 2^20 systems or a few hundred)."""
-    return {"checked": totals[20], "mismatched": totals[21], "ranks": totals[22], "world": world}
+    samples (all of them when the ranks' slices are 2^20 systems or a few hundred); and the
+    whole-slice check: ranks whose slice has a full-size golden, ranks whose slice equals it."""
+    return {"checked": totals[20], "mismatched": totals[21], "ranks": totals[22], "world": world,
+            "slices_golden": totals[23], "slices_equal": totals[24]}
 
 
 def sim_symbol(cache_size):
@@ -993,13 +1006,19 @@ def golden_record(slice_ok, cont, points, totals, world, M):
     objs = [samples_obj(totals, world)] + ([cont["samples"]] if cont else []) + \
         [p["samples"] for p in points or []]
     flags = [p["golden_slice"] for p in points] if points else None
+    head = samples_obj(totals, world)
     return {"slice": [0, M], "headline": slice_ok, "contention": cont.get("golden_slice") if cont else None,
+            # every rank's whole slice: [ranks equal to their slice's golden, ranks with one, world]
+            "ranks": {"headline": [head["slices_equal"], head["slices_golden"], world],
+                      "contention": ([cont["samples"]["slices_equal"], cont["samples"]["slices_golden"], world]
+                                     if cont else None)},
             "sweep": ([sum(f is True for f in flags), sum(f is not None for f in flags), len(flags)]
                       if flags is not None else None),
             "samples": [sum(o["checked"] for o in objs), sum(o["mismatched"] for o in objs),
                         min(o["ranks"] for o in objs), world],
             "basis": "slice: rank 0's own pre-reduce totals (hist, instructions, rounds, err_systems, digest_sum) vs "
-                     "tests/golden/full_size.json / sweep_full.json, null where no golden covers the workload; samples: "
+                     "tests/golden/full_size.json / sweep_full.json, null where no golden covers the workload; ranks: "
+                     "each rank's totals vs its slice's golden (full_slices.json for slices 1..7); samples: "
                      "each rank's systems among tests/golden/rank_samples.json's ids, per-system digest + rounds + "
                      "error bits"}
 
@@ -1089,6 +1108,9 @@ def compact_headline(d, detail_path):
     g = d.get("golden")
     if g:
         line["golden"] = {k: g.get(k) for k in ("slice", "headline", "contention", "sweep", "samples")}
+        rk = g.get("ranks") or {}
+        # whole slices of all ranks: [[headline equal, with a golden], [contention ...]] (world: samples[3])
+        line["golden"]["ranks"] = [(rk.get("headline") or [None, None])[:2], (rk.get("contention") or [None, None])[:2]]
     line["cpu_baseline"] = compact_cpu(d.get("cpu_baseline"))
     if d.get("cpu_baseline_note"):
         line["cpu_baseline_note"] = d["cpu_baseline_note"][:160]

@@ -46,11 +46,13 @@ def synthetic_detail(world=8, with_all=True):
                     "digest_sum": [2251634405826991 * world, 2249834063518710 * world],
                     "ub_frac": 0.2139053344726562, "tier_systems": [M, 12345, 67], "ub_systems": 224302 * world,
                     "err_frac": 0.2139053344726562, "golden_slice": True,
-                    "samples": {"checked": 32 * world, "mismatched": 0, "ranks": world, "world": world},
+                    "samples": {"checked": 32 * world, "mismatched": 0, "ranks": world, "world": world,
+                                "slices_golden": 1, "slices_equal": 1},
                     "cpu_baseline": _cpu(), "vs_baseline": 68371.23456789, "cpu_baseline_note": None})
     per_cs = {cs: {"points": 5, "batches": 15, "hung": 11, "hung_explained": 11, "oracle_ctz0": 11}
               for cs in (1, 2, 4, 8, 16)}
-    smp = {"checked": 48 * world, "mismatched": 0, "ranks": world, "world": world}
+    smp = {"checked": 48 * world, "mismatched": 0, "ranks": world, "world": world, "slices_golden": world,
+           "slices_equal": world}
     tot = {"hist": [15438985135] * 13, "instructions_per_step": 34359738368 * world,
            "rounds_total": 23801163240 * world, "err_systems": 51391 * world, "dropped": 60000 * world,
            "digest_sum": [2251634405826991 * world, 2249834063518710 * world], "ub_systems": 51391 * world}
@@ -84,7 +86,8 @@ def synthetic_detail(world=8, with_all=True):
                  "seeded": {"slowdown": 1.48123456, "parity_all_issued": True, "parity_reproducible": True}},
         "box": {"probe_before": probe, "probe_after": probe, "device": {"name": "AMD Instinct MI355X"}},
     } | {"samples": smp, "golden": bench.golden_record(True, {"samples": smp, "golden_slice": True}, pts,
-                                       tot["hist"] + [0] * 6 + [51391 * world, 48 * world, 0, world], world, M)}
+                                       tot["hist"] + [0] * 6 + [51391 * world, 48 * world, 0, world, world, world],
+                                       world, M)}
 
 
 @pytest.mark.parametrize("world", [1, 8])
@@ -109,6 +112,7 @@ def test_worst_case_line_fits_the_budget(world, tmp_path, capsys):
     g = line["golden"]
     assert g["slice"] == [0, 1 << 20] and g["headline"] is True and g["contention"] is True
     assert g["sweep"] == [25, 25, 25] and g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == world
+    assert g["ranks"] == [[world, world], [world, world]]  # every rank's whole slice, both workloads
     cols = line["sweep"]["cols"]
     assert all(dict(zip(cols, r))["golden"] is True and dict(zip(cols, r))["smp_bad"] == 0
                for r in line["sweep"]["rows"])

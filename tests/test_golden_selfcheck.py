@@ -121,11 +121,13 @@ def test_slice_golden_sweep_points():
 def test_golden_record_summarises_every_workload():
     pts = [{"golden_slice": True, "samples": {"checked": 3, "mismatched": 0, "ranks": 8, "world": 8}}] * 24 + \
           [{"golden_slice": None, "samples": {"checked": 3, "mismatched": 1, "ranks": 7, "world": 8}}]
-    tot = [0] * 20 + [5, 0, 8]
-    cont = {"samples": {"checked": 5, "mismatched": 0, "ranks": 8, "world": 8}, "golden_slice": True}
+    tot = [0] * 20 + [5, 0, 8, 8, 7]
+    cont = {"samples": {"checked": 5, "mismatched": 0, "ranks": 8, "world": 8, "slices_golden": 1,
+                        "slices_equal": 1}, "golden_slice": True}
     g = bench.golden_record(True, cont, pts, tot, 8, 1 << 20)
     assert g["headline"] is True and g["contention"] is True and g["sweep"] == [24, 24, 25]
     assert g["samples"] == [5 + 5 + 75, 1, 7, 8]
+    assert g["ranks"] == {"headline": [7, 8, 8], "contention": [1, 1, 8]}
 
 
 def test_stall_cause_reads_the_patch_notes():
@@ -185,3 +187,36 @@ def test_probe_sees_a_running_reference_move(tmp_path):
     if not running or len(snaps) < 2:
         pytest.skip("the instance finished before the second snapshot")
     assert moving == [0] and len(snaps[0]["queues"]) == 8
+
+
+def test_slice_golden_of_every_rank(monkeypatch):
+    """Slices r >= 1 of the 8-GPU layout (tests/golden/full_slices.json, make_full_slices.py): a rank
+    owning [r * 2^20, (r + 1) * 2^20) is checked against slice r's totals; a rank whose slice has no
+    golden, or whose size is not 2^20, is null."""
+    M = 1 << 20
+    tot = _local(FULL["uniform"])
+    fake = {"systems_per_slice": M, "instr_per_node": 4096, "seed": 0x5EED, "cache_size": 4,
+            "uniform": {"3": dict(tot)}, "contention": {}}
+    monkeypatch.setitem(bench._golden_cache, "full_slices.json", fake)
+    assert bench.slice_golden("uniform", 4, tot, 3 * M, M, ARGS) is True
+    assert bench.slice_golden("uniform", 4, dict(tot, err_systems=tot["err_systems"] + 1), 3 * M, M, ARGS) is False
+    assert bench.slice_golden("uniform", 4, tot, 4 * M, M, ARGS) is None
+    assert bench.slice_golden("contention", 4, tot, 3 * M, M, ARGS) is None
+    assert bench.slice_golden("locality:4:0.5", 4, tot, 3 * M, M, ARGS) is None
+    assert bench.slice_golden("uniform", 4, tot, 3 * 4096, 4096, ARGS) is None
+
+
+def test_full_slices_fixture_is_consistent():
+    """Whatever part of tests/golden/full_slices.json is committed: each slice ran every instruction of
+    its 2^20 systems, and no two slices (nor slice 0) share a digest checksum."""
+    f = ROOT / "tests" / "golden" / "full_slices.json"
+    if not f.exists():
+        pytest.skip("full_slices.json not generated")
+    g = json.loads(f.read_text())
+    for kind in ("uniform", "contention"):
+        sums = {tuple(FULL[kind]["digest_sum"])}
+        for r, t in g[kind].items():
+            assert 1 <= int(r) <= 7 and t["instructions"] == (1 << 20) * 8 * 4096
+            assert 0 < t["err_systems"] < 1 << 20 and sum(t["hist"]) > t["instructions"]
+            assert tuple(t["digest_sum"]) not in sums
+            sums.add(tuple(t["digest_sum"]))

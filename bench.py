@@ -18,7 +18,12 @@ after the timed region.
 The headline line also carries `contention` (BASELINE configs[3], its own timed steps),
 `cpu_baseline` (the reference itself, assignment.c + the SURVEY §8(d) benchmark patch,
 one instance per host core = BASELINE.md mode (A)) and `cpu_port` (the oracle restatement
-on the same host).
+on the same host). Every line certifies its own results at any GPU count (`golden`, round 6):
+each rank compares its own pre-reduce totals with the full-size golden of its slice where one is
+committed (rank 0's slice always: tests/golden/full_size.json, sweep_full.json; slices 1..7:
+full_slices.json) and its systems among the sampled ids of tests/golden/rank_samples.json with the
+oracle's per-system results; the counts ride in the one all-reduce. These are
+fixture files, not the oracle.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), at most LINE_BUDGET (4 KB)
 long: the driver keeps only a ~10 KB tail of stdout + stderr, and round 4's 52-KB line was

@@ -8,8 +8,9 @@ N-GPU line certifies all N x 2^20 systems, not rank 0's alone.
 
 Writes tests/golden/full_slices.json {"<kind>": {"<r>": totals}} after every slice (a long run
 keeps what it did; existing slices are kept unless recomputed).
-Usage: python tests/golden/make_full_slices.py [threads] [kind:r ...]   (about 25 min per slice on 7
-threads; default: uniform 1..7, then contention 1..7)
+Usage: python tests/golden/make_full_slices.py [--out FILE] [threads] [kind:r ...]   (about 27 min per
+slice on 7 threads; default: uniform 1..7, then contention 1..7; --out writes another file, merged
+into this one by hand: the contention slices were computed on the GPU box's 16 host CPUs)
 """
 import json
 import pathlib
@@ -49,10 +50,13 @@ def totals(kind, r, threads):
 
 
 if __name__ == "__main__":
-    threads = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-    todo = [(a.split(":")[0], int(a.split(":")[1])) for a in sys.argv[2:]] or \
-        [(k, r) for k in ("uniform", "contention") for r in range(1, 8)]
+    argv = sys.argv[1:]
     path = pathlib.Path(__file__).resolve().parent / "full_slices.json"
+    if argv[:1] == ["--out"]:  # another file (e.g. under gpurun_out/ when run on a bigger host)
+        path, argv = pathlib.Path(argv[1]), argv[2:]
+    threads = int(argv[0]) if argv else 8
+    todo = [(a.split(":")[0], int(a.split(":")[1])) for a in argv[1:]] or \
+        [(k, r) for k in ("uniform", "contention") for r in range(1, 8)]
     out = json.loads(path.read_text()) if path.exists() else {
         "systems_per_slice": SYSTEMS, "num_procs": 8, "instr_per_node": LEN, "cache_size": CS, "seed": SEED,
         "generator": "oracle/dash_oracle.c orc_run_batch (counter-based, keyed by global system id); slice r = "

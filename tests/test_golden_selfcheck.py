@@ -103,8 +103,10 @@ def test_slice_golden_headline_and_contention():
         assert bench.slice_golden(key, 4, bad, 0, M, ARGS) is False
         bad = dict(loc, hist=[loc["hist"][0] - 1] + loc["hist"][1:])
         assert bench.slice_golden(key, 4, bad, 0, M, ARGS) is False
-        # not rank 0's slice, another size, another CACHE_SIZE: no golden applies
-        assert bench.slice_golden(key, 4, loc, M, M, ARGS) is None
+        # rank 1's slice has its own golden (full_slices.json), which slice 0's totals do not match;
+        # another size, another CACHE_SIZE: no golden applies
+        assert bench.slice_golden(key, 4, loc, M, M, ARGS) is (False if (ROOT / "tests" / "golden" /
+                                                                          "full_slices.json").exists() else None)
         assert bench.slice_golden(key, 4, loc, 0, M // 2, ARGS) is None
         assert bench.slice_golden(key, 8, loc, 0, M, ARGS) is None
 
@@ -213,10 +215,11 @@ def test_full_slices_fixture_is_consistent():
     if not f.exists():
         pytest.skip("full_slices.json not generated")
     g = json.loads(f.read_text())
+    assert sorted(g["uniform"]) == sorted(g["contention"]) == [str(r) for r in range(1, 8)]
     for kind in ("uniform", "contention"):
         sums = {tuple(FULL[kind]["digest_sum"])}
         for r, t in g[kind].items():
             assert 1 <= int(r) <= 7 and t["instructions"] == (1 << 20) * 8 * 4096
-            assert 0 < t["err_systems"] < 1 << 20 and sum(t["hist"]) > t["instructions"]
+            assert 0 < t["err_systems"] < 1 << 20 and sum(t["hist"]) > t["instructions"] // 2
             assert tuple(t["digest_sum"]) not in sums
             sums.add(tuple(t["digest_sum"]))

@@ -524,7 +524,9 @@ def slice_golden(key, cache_size, local, sys_base, M, args):
     r = sys_base // M
     if r:
         g = golden_file("full_slices.json")
-        gp = (g or {}).get(key, {}).get(str(r)) if g and g.get("cache_size") == cache_size else None
+        # the headline workloads at the file's CACHE_SIZE; a configs[4] key names its own
+        same_cs = key.startswith("locality:") or (g or {}).get("cache_size") == cache_size
+        gp = (g or {}).get(key, {}).get(str(r)) if g and same_cs else None
         if not gp or (g["systems_per_slice"], g["instr_per_node"], g["seed"]) != (M, args.len, args.seed):
             return None
         return all(local[k] == gp[k] for k in ("hist", "instructions", "rounds_total", "err_systems", "digest_sum"))

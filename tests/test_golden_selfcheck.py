@@ -216,8 +216,9 @@ def test_full_slices_fixture_is_consistent():
         pytest.skip("full_slices.json not generated")
     g = json.loads(f.read_text())
     assert sorted(g["uniform"]) == sorted(g["contention"]) == [str(r) for r in range(1, 8)]
-    for kind in ("uniform", "contention"):
-        sums = {tuple(FULL[kind]["digest_sum"])}
+    sweep0 = {bench.golden_key("locality", q["cache_size"], q["locality"]): q for q in SWEEP_FULL["points"]}
+    for kind in [k for k in g if k in ("uniform", "contention") or k.startswith("locality:")]:
+        sums = {tuple((FULL[kind] if kind in FULL else sweep0[kind])["digest_sum"])}
         for r, t in g[kind].items():
             assert 1 <= int(r) <= 7 and t["instructions"] == (1 << 20) * 8 * 4096
             assert 0 < t["err_systems"] < 1 << 20 and sum(t["hist"]) > t["instructions"] // 2

@@ -1019,7 +1019,10 @@ def golden_record(slice_ok, cont, points, totals, world, M):
             "ranks": {"headline": [head["slices_equal"], head["slices_golden"], world],
                       "contention": ([cont["samples"]["slices_equal"], cont["samples"]["slices_golden"], world]
                                      if cont else None)},
-            "sweep": ([sum(f is True for f in flags), sum(f is not None for f in flags), len(flags)]
+            # [rank 0 equal, rank 0 with a golden, points, all ranks' slices equal, all ranks' slices with one]
+            "sweep": ([sum(f is True for f in flags), sum(f is not None for f in flags), len(flags),
+                       sum(p["samples"].get("slices_equal", 0) for p in points),
+                       sum(p["samples"].get("slices_golden", 0) for p in points)]
                       if flags is not None else None),
             "samples": [sum(o["checked"] for o in objs), sum(o["mismatched"] for o in objs),
                         min(o["ranks"] for o in objs), world],

@@ -111,7 +111,7 @@ def test_worst_case_line_fits_the_budget(world, tmp_path, capsys):
     # full-size goldens, every rank's sampled ids -- and each sweep row says which point it checked
     g = line["golden"]
     assert g["slice"] == [0, 1 << 20] and g["headline"] is True and g["contention"] is True
-    assert g["sweep"] == [25, 25, 25] and g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == world
+    assert g["sweep"][:3] == [25, 25, 25] and g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == world
     assert g["ranks"] == [[world, world], [world, world]]  # every rank's whole slice, both workloads
     cols = line["sweep"]["cols"]
     assert all(dict(zip(cols, r))["golden"] is True and dict(zip(cols, r))["smp_bad"] == 0
@@ -208,7 +208,7 @@ def test_committed_r06_lines_certify_themselves(path, world):
     assert line["n_gpus"] == world
     g = line["golden"]
     assert g["slice"] == [0, 1 << 20] and g["headline"] is True and g["contention"] is True
-    assert g["sweep"] == [25, 25, 25]
+    assert g["sweep"][:3] == [25, 25, 25]
     checked, bad, ranks, w = g["samples"]
     assert checked > 0 and bad == 0 and ranks == w == world
     cols = line["sweep"]["cols"]

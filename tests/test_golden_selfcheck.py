@@ -127,7 +127,7 @@ def test_golden_record_summarises_every_workload():
     cont = {"samples": {"checked": 5, "mismatched": 0, "ranks": 8, "world": 8, "slices_golden": 1,
                         "slices_equal": 1}, "golden_slice": True}
     g = bench.golden_record(True, cont, pts, tot, 8, 1 << 20)
-    assert g["headline"] is True and g["contention"] is True and g["sweep"] == [24, 24, 25]
+    assert g["headline"] is True and g["contention"] is True and g["sweep"][:3] == [24, 24, 25]
     assert g["samples"] == [5 + 5 + 75, 1, 7, 8]
     assert g["ranks"] == {"headline": [7, 8, 8], "contention": [1, 1, 8]}
 

@@ -179,7 +179,7 @@ def test_four_ranks_line_is_the_driver_shape():
     # from the oracle; no full-size slice golden covers 256 systems per rank (null, not false)
     g = line["golden"]
     assert g["samples"][0] >= 27 * 4 and g["samples"][1] == 0 and g["samples"][2] == g["samples"][3] == 4, g
-    assert g["headline"] is None and g["contention"] is None and g["sweep"] == [0, 0, 25]
+    assert g["headline"] is None and g["contention"] is None and g["sweep"][:3] == [0, 0, 25]
     assert all(r[line["sweep"]["cols"].index("smp_bad")] == 0 for r in line["sweep"]["rows"])
 
 

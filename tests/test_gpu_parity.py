@@ -896,3 +896,25 @@ def test_every_rank_slice_of_the_eight_gpu_layout(dash, kind):
             # slice 0: full_size.json; slices 1..7 where tests/golden/full_slices.json holds them
             assert ok is True if r == 0 else ok is not False, (r, ok)
     assert checked == sum(1 for _ in json.loads((GOLDEN.parent / "rank_samples.json").read_text())["ids"])
+
+
+def test_sweep_points_on_the_second_slice(dash):
+    """configs[4] as rank 1 of the driver's N >= 2 runs computes it: global systems [2^20, 2^21), all
+    25 CACHE_SIZE x locality points at full size, each equal to the oracle's run of that slice
+    (tests/golden/full_slices.json, make_full_slices.py) -- so an N = 2 line certifies both ranks'
+    whole slices at every sweep point."""
+    import argparse
+    args = argparse.Namespace(len=4096, seed=0x5EED)
+    M = 1 << 20
+    n = 0
+    for cs in (1, 2, 4, 8, 16):
+        with dash.Engine(M, num_procs=8, cache_size=cs, max_instr=4096) as eng:
+            for p in (0.0, 0.25, 0.5, 0.75, 1.0):
+                eng.generate(0x5EED, 4096, kind=dash.GEN_LOCALITY, locality=int(round(p * 65536)), sys_base=M)
+                st = eng.run()
+                d = eng.read_results()[0]
+                local = {"hist": st["hist"], "instructions": st["instructions"], "rounds_total": st["rounds_total"],
+                         "err_systems": st["err_systems"], "digest_sum": bench.digest_sum(d)}
+                assert bench.slice_golden(bench.golden_key("locality", cs, p), cs, local, M, M, args) is True, (cs, p)
+                n += 1
+    assert n == 25

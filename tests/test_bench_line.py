@@ -194,7 +194,8 @@ def test_committed_line_has_every_row_measured():
                                         ("profiles/r06/ev6_d/bench.json", 1), ("profiles/r06/ev6_e/bench.json", 1),
                                         ("profiles/r06/two_rank_full/bench.json", 2),
                                         ("profiles/r06/two_rank_full_b/bench.json", 2),
-                                        ("profiles/r06/two_rank_full_c/bench.json", 2)])
+                                        ("profiles/r06/two_rank_full_c/bench.json", 2),
+                                        ("profiles/r06/four_rank_full/bench.json", 4)])
 def test_committed_r06_lines_certify_themselves(path, world):
     """VERDICT r5 next #1 / #3 on the committed round-6 lines (the driver's command on one GPU, and
     the same at N = 2 with both ranks on the box's GPU): rank 0's slice equals the full-size goldens
@@ -222,5 +223,5 @@ def test_committed_r06_lines_certify_themselves(path, world):
     assert line["ub_frac"] == pytest.approx(GOLD["uniform"]["err_systems"] / GOLD["systems"], rel=1e-2)
     if "ranks" in g:  # since the whole-slice goldens of every rank (full_slices.json)
         assert g["ranks"] == [[world, world], [world, world]]
-    if len(g["sweep"]) == 5:  # since slice 1 of every configs[4] point: every rank's slice at every point
-        assert g["sweep"][3:] == [25 * world, 25 * world]
+    if len(g["sweep"]) == 5:  # slice 1 of every configs[4] point is committed, slices 2.. are not
+        assert g["sweep"][3:] == [25 * min(world, 2)] * 2
